@@ -1,0 +1,81 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.  ctypes binding of oracle/mmsbm_oracle.c.
+
+Array-level view of the reference path (`src/TrigenicInteractionPredictor.py`
+:952-974 loglik, :984-1043 EM step, :530-547 prediction), bit-identical to
+`oracle/mmsbm_oracle.py`.  Layouts: ids int32[E][3], counts int32[E][R],
+theta f64[P][K], pr f64[K][K][K][R] (the reference's nesting).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libmmsbm_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        P_i32 = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+        P_f64 = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        L.oracle_loglik.restype = ctypes.c_double
+        L.oracle_loglik.argtypes = [ctypes.c_int64, P_i32, P_i32, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_double, P_f64, P_f64]
+        L.oracle_make_iteration.restype = ctypes.c_int
+        L.oracle_make_iteration.argtypes = [ctypes.c_int64, P_i32, P_i32, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_double, P_f64, P_f64]
+        L.oracle_predict.restype = None
+        L.oracle_predict.argtypes = [ctypes.c_int64, P_i32, ctypes.c_int, ctypes.c_int,
+                                     P_f64, P_f64, P_f64]
+        _lib = L
+    return _lib
+
+
+def links_to_arrays(links: dict, R: int = 2):
+    """`links` dict ("i_j_k" -> [n0, n1]) in insertion order -> (ids, counts)."""
+    E = len(links)
+    ids = np.empty((E, 3), dtype=np.int32)
+    counts = np.empty((E, R), dtype=np.int32)
+    for e, (key, n) in enumerate(links.items()):
+        ids[e] = [int(s) for s in key.split("_")]
+        counts[e] = n[:R]
+    return ids, counts
+
+
+def loglik(ids, counts, theta, pr, eps=1e-10):
+    K = theta.shape[1]
+    R = counts.shape[1]
+    return lib().oracle_loglik(ids.shape[0], ids, counts, K, R, eps,
+                               np.ascontiguousarray(theta), np.ascontiguousarray(pr))
+
+
+def make_iteration(ids, counts, theta, pr, eps=1e-10):
+    """Returns new (theta, pr); raises ZeroDivisionError like :1018."""
+    theta = np.array(theta, dtype=np.float64, copy=True, order="C")
+    pr = np.array(pr, dtype=np.float64, copy=True, order="C")
+    P, K = theta.shape
+    R = counts.shape[1]
+    rc = lib().oracle_make_iteration(ids.shape[0], ids, counts, P, K, R, eps, theta, pr)
+    if rc != 0:
+        raise ZeroDivisionError("float division by zero")
+    return theta, pr
+
+
+def predict(ids, theta, pr):
+    K = theta.shape[1]
+    out = np.empty(ids.shape[0], dtype=np.float64)
+    lib().oracle_predict(ids.shape[0], np.ascontiguousarray(ids), K, pr.shape[-1],
+                         np.ascontiguousarray(theta), np.ascontiguousarray(pr), out)
+    return out

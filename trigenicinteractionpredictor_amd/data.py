@@ -1,0 +1,166 @@
+"""Synthetic fold files in the reference's on-disk format.
+
+The reference's real folds (`data/DATA_FOLDS/{train,test}{0-4}.dat`) are Git-LFS
+pointers, so every configuration is stood in for by a generated fold with the
+same file format: one line per link, ``name1_name2_name3\\t<r>\\n`` with the three
+gene names sorted (format written by `src/TrigenicInteractionPredictor.py:486-491`
+and `:516-521`, read by `get_traintest` `:321-423`).
+
+Genes are named ``g%05d`` (zero padded, so string order == numeric order),
+positives are Bernoulli(``pos_frac``) and the first ``test_frac`` of the
+non-coverage triples go to the test file.  Every gene is placed in at least one
+train triple: a gene seen only in the test file makes the reference's
+``make_iteration`` divide by a zero degree (`:1016-1018`).
+"""
+from __future__ import annotations
+
+import os
+import random
+from dataclasses import dataclass
+
+import numpy as np
+
+__all__ = ["FoldSpec", "FOLD0", "write_fold", "gene_name"]
+
+
+def gene_name(idx: int) -> str:
+    return "g%05d" % idx
+
+
+@dataclass(frozen=True)
+class FoldSpec:
+    """Shape of a synthetic fold.  ``E`` counts unique triples (train + test)."""
+
+    P: int
+    E: int
+    seed: int = 7
+    pos_frac: float = 0.05
+    test_frac: float = 0.2
+    multi_frac: float = 0.0   # train links given 1..3 extra copies of their line
+    both_frac: float = 0.0    # train links given one extra line with the other rating
+    dup_frac: float = 0.0     # triples with a repeated gene, e.g. a_a_c
+
+
+# "fold0 stand-in", sized from the LFS byte counts
+# (train0.dat 1,793,824 B + test0.dat 448,744 B at ~25 B/line).
+FOLD0 = FoldSpec(P=1500, E=90000, seed=7)
+
+
+def _line(names, r) -> str:
+    return "_".join(names) + "\t" + str(r) + "\n"
+
+
+def _python_triples(spec: FoldSpec, rng: random.Random):
+    P = spec.P
+    seen = set()
+    cover = []
+    perm = list(range(P))
+    rng.shuffle(perm)
+    for s in range(0, P, 3):
+        tri = perm[s:s + 3]
+        while len(tri) < 3:
+            g = rng.randrange(P)
+            if g not in tri:
+                tri.append(g)
+        key = tuple(sorted(tri))
+        if key not in seen:
+            seen.add(key)
+            cover.append(key)
+    rest = []
+    while len(cover) + len(rest) < spec.E:
+        if spec.dup_frac and rng.random() < spec.dup_frac:
+            a, c = rng.sample(range(P), 2)
+            key = tuple(sorted((a, a, c)))
+        else:
+            key = tuple(sorted(rng.sample(range(P), 3)))
+        if key in seen:
+            continue
+        seen.add(key)
+        rest.append(key)
+    return cover, rest
+
+
+def _numpy_triples(spec: FoldSpec):
+    """Vectorised variant for large E (10M-link stress config)."""
+    P, E = spec.P, spec.E
+    rs = np.random.default_rng(spec.seed)
+    perm = rs.permutation(P)
+    nfull = P // 3
+    cover = np.sort(perm[: nfull * 3].reshape(nfull, 3), axis=1)
+    if P % 3:
+        tail = list(perm[nfull * 3:])
+        others = [g for g in rs.permutation(P) if g not in tail][: 3 - len(tail)]
+        cover = np.vstack([cover, np.sort(np.array(tail + others))[None, :]])
+    enc = lambda t: (t[:, 0].astype(np.int64) * P + t[:, 1]) * P + t[:, 2]
+    cover_codes = np.unique(enc(cover))
+    need = E - cover_codes.size
+    codes = np.empty(0, dtype=np.int64)
+    while codes.size < need:
+        m = int((need - codes.size) * 1.1) + 1024
+        t = rs.integers(0, P, size=(m, 3))
+        t = t[(t[:, 0] != t[:, 1]) & (t[:, 0] != t[:, 2]) & (t[:, 1] != t[:, 2])]
+        t.sort(axis=1)
+        c = np.unique(enc(t))
+        c = c[~np.isin(c, cover_codes)]
+        codes = np.unique(np.concatenate([codes, c]))
+    codes = rs.permutation(codes)[:need]
+    dec = lambda c: np.stack([c // (P * P), (c // P) % P, c % P], axis=1)
+    return dec(cover_codes), dec(codes), rs
+
+
+def write_fold(spec: FoldSpec, train_path: str, test_path: str) -> tuple[int, int]:
+    """Write a synthetic train/test fold pair; returns (#train lines, #test lines)."""
+    if spec.E >= 1_000_000:
+        return _write_fold_numpy(spec, train_path, test_path)
+    rng = random.Random(spec.seed)
+    cover, rest = _python_triples(spec, rng)
+    n_test = int(spec.E * spec.test_frac)
+    n_test = min(n_test, len(rest))
+    test, train_rest = rest[:n_test], rest[n_test:]
+    train = cover + train_rest
+    rng.shuffle(train)
+    rating = {}
+    for key in train + test:
+        rating[key] = 1 if rng.random() < spec.pos_frac else 0
+    names = lambda key: sorted(gene_name(g) for g in key)
+    train_lines = [_line(names(k), rating[k]) for k in train]
+    extra = []
+    for k in train:
+        if spec.multi_frac and rng.random() < spec.multi_frac:
+            extra += [_line(names(k), rating[k])] * rng.randint(1, 3)
+        if spec.both_frac and rng.random() < spec.both_frac:
+            extra.append(_line(names(k), 1 - rating[k]))
+    rng.shuffle(extra)
+    train_lines += extra
+    test_lines = [_line(names(k), rating[k]) for k in test]
+    for path, lines in ((train_path, train_lines), (test_path, test_lines)):
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        with open(path, "w", encoding="utf-8") as f:
+            f.writelines(lines)
+    return len(train_lines), len(test_lines)
+
+
+def _write_fold_numpy(spec: FoldSpec, train_path: str, test_path: str):
+    cover, rest, rs = _numpy_triples(spec)
+    n_test = min(int(spec.E * spec.test_frac), rest.shape[0])
+    test = rest[:n_test]
+    train = np.vstack([cover, rest[n_test:]])
+    train = train[rs.permutation(train.shape[0])]
+    width = len(gene_name(spec.P - 1))
+
+    def dump(path, tri):
+        r = (rs.random(tri.shape[0]) < spec.pos_frac).astype(np.int64)
+        names = np.char.add("g", np.char.zfill(tri.astype(str), width - 1))
+        lines = np.char.add(np.char.add(np.char.add(names[:, 0], "_"),
+                                        np.char.add(names[:, 1], "_")),
+                            np.char.add(names[:, 2], np.char.add("\t", r.astype(str))))
+        with open(path, "w", encoding="utf-8") as f:
+            chunk = 1 << 20
+            for s in range(0, lines.size, chunk):
+                f.write("\n".join(lines[s:s + chunk].tolist()))
+                f.write("\n")
+
+    dump(train_path, train)
+    dump(test_path, test)
+    return int(train.shape[0]), int(test.shape[0])
