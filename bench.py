@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark: EM-iterations/sec on the fold0 stand-in, K=10 (BASELINE.json metric, configs[1]).
+
+A "step" is one EM iteration (`Model.make_iteration`, src/TrigenicInteractionPredictor.py
+:984-1043) of every sample resident on a GPU over the fold0-shaped synthetic train set
+(P=1,500 genes, 72,000 train links, 18,000 test links).  Samples
+(independent EM restarts, :1253) shard across ranks with no data-path collective (weak
+scaling); the final log-likelihoods are gathered over RCCL at the end (:1262-1279 analogue).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--K 10] [--samples 1]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  `roofline` is measured live with HIP events around every
+E-step launch in the timed region (the launches' own stream).  `cpu_baseline` times the
+pure-Python CPU restatement of the reference path (oracle/, test infrastructure) on a bounded
+sample of the same workload, on this host, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import random
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector: 256 CU x 128 FLOP/clk x 2.4 GHz (spec)
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--K", type=int, default=10)
+    ap.add_argument("--samples", type=int, default=1, help="samples (restarts) per GPU")
+    ap.add_argument("--P", type=int, default=1500)
+    ap.add_argument("--E", type=int, default=90000, help="unique triples, train + test")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def make_fold(P, E, rank):
+    from trigenicinteractionpredictor_amd.data import FoldSpec, write_fold
+    d = tempfile.mkdtemp(prefix="mmsbm_bench_r%d_" % rank)
+    tr, te = os.path.join(d, "train0.dat"), os.path.join(d, "test0.dat")
+    write_fold(FoldSpec(P=P, E=E, seed=7), tr, te)
+    return tr, te
+
+
+def cpu_baseline(train, test, K, seed, seconds):
+    """Pure-Python restatement of :984-1043 (bit-identical to the reference under CPython).
+    The per-link loop (:987-1012, all of the cost) is timed on the first n links so that the
+    sample takes ~`seconds` and scaled to all links; the M-step (:1016-1043) is timed whole."""
+    import contextlib
+    import io
+    from oracle.mmsbm_oracle import OracleModel
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = OracleModel()
+        m.get_traintest(train, test)
+    random.seed(seed)
+    m.initialize_parameters(K)
+    items = list(m.links.items())
+    E = len(items)
+    t0 = time.perf_counter()
+    m.accumulate(items[:32])
+    per_link = (time.perf_counter() - t0) / 32
+    n = max(32, min(E, int(seconds / per_link)))
+    t0 = time.perf_counter()
+    m.accumulate(items[:n])
+    t_loop = time.perf_counter() - t0
+    full_deg = [0] * m.P
+    for key in m.links:
+        for s in key.split("_"):
+            full_deg[int(s)] += 1
+    nth = [[1.0] * K for _ in range(m.P)]
+    npr = [[[[0.5] * m.R for _ in range(K)] for _ in range(K)] for _ in range(K)]
+    t0 = time.perf_counter()
+    m.finish(nth, npr, full_deg)
+    t_fin = time.perf_counter() - t0
+    full_iter_s = t_loop * E / n + t_fin
+    return {"value": 1.0 / full_iter_s, "unit": "EM-iterations/s", "cores": 1, "kind": "port",
+            "sample": "oracle OracleModel.make_iteration (pure-Python restatement of :984-1043), "
+                      "per-link loop timed on %d of %d train links (%.1f s) and scaled x%.2f, "
+                      "M-step timed whole (%.3f s); K=%d, %s %s, 1 process -> %.1f s/iter" % (
+                          n, E, t_loop, E / n, t_fin, K, platform.python_implementation(),
+                          platform.python_version(), full_iter_s)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from trigenicinteractionpredictor_amd import EMEngine, Model
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays, build_obs
+
+    train, test = make_fold(args.P, args.E, rank)
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        host = Model()
+        host.get_traintest(train, test)
+    K, B = args.K, args.samples
+    # restart sharding: global sample s = rank*B + b; one RNG stream seeded once, like :1149/:1260
+    random.seed(args.seed)
+    thetas, prs = [], []
+    for s in range((rank + 1) * B):
+        host.initialize_parameters(K)
+        if s >= rank * B:
+            thetas.append(np.array(host._theta))
+            prs.append(np.array(host._pr))
+    eng = EMEngine(K, host.P, B=B, device=dev)
+    ids, counts = links_to_arrays(host.links)
+    eng.set_links(0, ids, counts)
+    eng.set_links(1, *links_to_arrays(host.test_links))
+    eng.upload(np.stack(thetas), np.stack(prs))
+    E_obs = int(build_obs(ids, counts).n_obs)
+
+    eng.iterate(args.warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    eng.timing(True)
+    t0 = time.perf_counter()
+    eng.iterate(args.steps)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    est_ms, est_n = eng.timing_result("estep")
+    ms_ms, _ = eng.timing_result("mstep")
+    eng.timing(False)
+    elapsed = t1 - t0
+    L = torch.from_numpy(eng.loglik(0)).to(dev)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        gathered = [torch.empty_like(L) for _ in range(world)]
+        dist.all_gather(gathered, L)       # RCCL gather of final likelihoods
+        L_all = torch.cat(gathered).cpu().numpy()
+    else:
+        L_all = L.cpu().numpy()
+
+    if rank == 0:
+        iters_total = args.steps * B * world
+        value = iters_total / elapsed
+        # roofline of the dominant kernel (E-step), per launch; SURVEY.md §8d figures
+        est_avg_s = est_ms / 1e3 / max(est_n, 1)
+        flops = 8.0 * K ** 3 * E_obs * B
+        hbm_bytes = (16.0 * E_obs + 16.0 * host.P * K + 24.0 * K ** 3 * 2) * B
+        achieved_tf = flops / est_avg_s / 1e12
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_estep_K%d.json" % K)
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                rec = json.load(f)
+            if rec.get("E_obs") == E_obs and rec.get("B") == B:
+                traffic = rec.get("hbm_bytes_per_launch")
+        line = {
+            "metric": "EM-iterations/sec + final log-likelihood, fold0 K=%d" % K,
+            "value": value,
+            "unit": "EM-iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic fold0 stand-in (real fold0 is a Git-LFS pointer)",
+            "config": {"workload": "fold0 stand-in, K=%d, %d sample(s)/GPU" % (K, B), "K": K,
+                       "P": host.P, "E_train": len(host.links), "E_test": len(host.test_links),
+                       "E_obs": E_obs, "samples_per_gpu": B, "parallelism": "restart-sharded x%d" % world},
+            "final_loglik": float(L_all[0]),
+            "final_loglik_best": float(L_all.max()),
+            "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "kernel": "estep_kernel<%d>" % K, "avg_launch_us": est_avg_s * 1e6,
+                         "algorithmic_flops_per_launch": flops,
+                         "hbm": {"achieved": hbm_bytes / est_avg_s / 1e9, "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": hbm_bytes / est_avg_s / 1e9 / HBM_PEAK_GBS,
+                                 "algorithmic_bytes_per_launch": hbm_bytes}},
+            "kernel_us": {"estep": est_avg_s * 1e6, "mstep": ms_ms * 1e3 / max(est_n, 1)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(train, test, K, args.seed, args.cpu_baseline_seconds)
+            line["vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
