@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true", help="do not time kernels (overhead probe)")
     return ap.parse_args()
 
 
@@ -141,7 +142,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    eng.timing(True)
+    eng.timing(not args.no_events)
     t0 = time.perf_counter()
     eng.iterate(args.steps)
     torch.cuda.synchronize(dev)
@@ -167,7 +168,7 @@ def main():
         iters_total = args.steps * B * world
         value = iters_total / elapsed
         # roofline of the dominant kernel (E-step), per launch; SURVEY.md §8d figures
-        est_avg_s = est_ms / 1e3 / max(est_n, 1)
+        est_avg_s = est_ms / 1e3 / est_n if est_n else float("nan")
         flops = 8.0 * K ** 3 * E_obs * B
         hbm_bytes = (16.0 * E_obs + 16.0 * host.P * K + 24.0 * K ** 3 * 2) * B
         achieved_tf = flops / est_avg_s / 1e12

@@ -50,6 +50,7 @@ namespace {
 constexpr int TILE = MMSBM_TILE;
 constexpr int MAX_R = 8;
 constexpr int LDS_BUDGET = 64 * 1024;
+constexpr int MIN_TS = 64;  // smallest E-step tile (observations per workgroup)
 
 thread_local std::string g_err;
 
@@ -83,26 +84,17 @@ constexpr int pick_nb(int K) {
   return (2 * best >= cap) ? best : cap;
 }
 
-template <int K>
-struct Tiling {
+// Phase-B (S accumulation) tiling for NT threads: lane = (cell block, link group).
+template <int K, int NT>
+struct SPlan {
   static constexpr int K3 = K * K * K;
-  static constexpr int KP = (K + 1) & ~1;  // LDS row stride in doubles (16-B aligned rows)
   static constexpr int NB = pick_nb(K);    // b-chunk per lane
   static constexpr int NBC = (K + NB - 1) / NB;
   static constexpr int NBLK = K * NBC;     // cell blocks (a, b-chunk, all g)
-  static constexpr int NSETS = (NBLK + TILE - 1) / TILE;
-  static constexpr int LG_RAW = NBLK >= TILE ? 1 : TILE / NBLK;
+  static constexpr int NSETS = (NBLK + NT - 1) / NT;
+  static constexpr int LG_RAW = NBLK >= NT ? 1 : NT / NBLK;
   static constexpr int LG_RED = 2 * (LDS_BUDGET / (8 * K3)) + 1;  // keep the reduction in budget
   static constexpr int LG = LG_RAW < LG_RED ? LG_RAW : LG_RED;    // link groups
-  static constexpr int LINK_BYTES = 3 * KP * 8;
-  static constexpr int CH = (TILE * LINK_BYTES <= LDS_BUDGET)       ? TILE
-                            : ((TILE / 2) * LINK_BYTES <= LDS_BUDGET) ? TILE / 2
-                                                                      : TILE / 4;
-  static constexpr int STAGE_BYTES = CH * LINK_BYTES;
-  static constexpr int RED_BYTES = (LG / 2) * K3 * 8;
-  static constexpr int LDS_BYTES = (STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES);
-  static_assert(LDS_BYTES <= LDS_BUDGET, "phase-B LDS over budget");
-  static_assert(CH * LINK_BYTES <= LDS_BUDGET, "staging chunk over budget");
 };
 
 // Wave64 butterfly sum in a fixed order (bitwise reproducible).
@@ -150,9 +142,11 @@ __device__ __forceinline__ double phase_a(const double* __restrict__ th, const d
     double wc[K];
 #pragma unroll
     for (int g = 0; g < K; ++g) wc[g] = 0.0;
+    double ta_next = ri[0];
 #pragma unroll 1
     for (int a = 0; a < K; ++a) {
-      const double ta = ri[a];
+      const double ta = ta_next;
+      ta_next = ri[a + 1 < K ? a + 1 : a];  // prefetch: its latency hides under this iteration
       const double* __restrict__ pa = p + a * K2;
       double y = 0.0;
 #pragma unroll
@@ -176,9 +170,11 @@ __device__ __forceinline__ double phase_a(const double* __restrict__ th, const d
     }
   } else {
     // two passes keep the live set at 3K (pass 1) / 2K (pass 2) doubles
+    double ta_next = ri[0];
 #pragma unroll 1
     for (int a = 0; a < K; ++a) {
-      const double ta = ri[a];
+      const double ta = ta_next;
+      ta_next = ri[a + 1 < K ? a + 1 : a];
       const double* __restrict__ pa = p + a * K2;
       double y = 0.0;
 #pragma unroll
@@ -197,9 +193,11 @@ __device__ __forceinline__ double phase_a(const double* __restrict__ th, const d
     double wc[K];
 #pragma unroll
     for (int g = 0; g < K; ++g) wc[g] = 0.0;
+    ta_next = ri[0];
 #pragma unroll 1
     for (int a = 0; a < K; ++a) {
-      const double ta = ri[a];
+      const double ta = ta_next;
+      ta_next = ri[a + 1 < K ? a + 1 : a];
       const double* __restrict__ pa = p + a * K2;
 #pragma unroll
       for (int b = 0; b < K; ++b) {
@@ -229,9 +227,11 @@ __device__ __forceinline__ double contract(const double* __restrict__ th, const 
     tk[g] = rk[g];
   }
   double dsum = 0.0;
+  double ta_next = ri[0];
 #pragma unroll 1
   for (int a = 0; a < K; ++a) {
-    const double ta = ri[a];
+    const double ta = ta_next;
+    ta_next = ri[a + 1 < K ? a + 1 : a];
     const double* __restrict__ pa = p + a * K2;
     double y = 0.0;
 #pragma unroll
@@ -247,50 +247,241 @@ __device__ __forceinline__ double contract(const double* __restrict__ th, const 
 }
 
 // ------------------------------------------------------------------------------------------
-// E-step: grid (ntiles, B), block TILE.
+// E-step plan.  TS observations per workgroup, H lanes per observation (NT = TS*H threads).
+//   K <= 12: p_r is staged in LDS once per workgroup and read with ds_read_b128 (broadcast);
+//            H = 2: the two lanes of an observation split the a-range and exchange their
+//            Z / W / d partials with one lane swap (2x the waves of one-lane-per-observation:
+//            a fold0-sized problem otherwise leaves ~1 wave per SIMD to hide all latency).
+//   K > 12:  p_r streams through the scalar cache (SGPR operands), H = 1.
+// LDS: Ps [K slabs of K*KP, second half shifted by 16 B so the two lanes' reads hit distinct
+//      banks], Ri/Rj/Rk [TS][RS] theta rows of every observation (RS = 2 mod 4 doubles:
+//      conflict-free 16-lane ds_read_b128), Cv [TS] c = n/d, red (phase-B reduction, aliases
+//      the rows once accumulation is done), 8 doubles of block-sum scratch.
 // ------------------------------------------------------------------------------------------
-template <int K>
-__global__ __launch_bounds__(TILE) void estep_kernel(
+template <int K, int TS>
+struct EPlan {
+  static constexpr bool STAGE_P = K <= 12;
+  static constexpr int H = STAGE_P ? 2 : 1;
+  static constexpr int NT = TS * H;
+  using S = SPlan<K, NT>;
+  static constexpr int K3 = K * K * K;
+  static constexpr int KP = (K + 1) & ~1;
+  static constexpr int KH = (K + H - 1) / H;   // a-range per lane
+  static constexpr int RS = (KP % 4 == 2) ? KP : KP + 2;
+  static constexpr int P_DBL = STAGE_P ? K * K * KP + 2 : 0;
+  static constexpr int CS_DBL = STAGE_P ? TS * 3 * K : 0;  // contrib rows, written out coalesced
+  static constexpr int ROWS_DBL = 3 * TS * RS;
+  static constexpr int RED_DBL = (S::LG / 2) * K3;
+  static constexpr int BODY_DBL = ROWS_DBL + TS > RED_DBL ? ROWS_DBL + TS : RED_DBL;
+  static constexpr int LDS_BYTES = (P_DBL + CS_DBL + BODY_DBL + 8) * 8;
+  static constexpr bool FITS = LDS_BYTES <= LDS_BUDGET;
+  __device__ static constexpr int slab(int a) { return a * K * KP + (a >= KH ? 2 : 0); }
+};
+
+// Phase A, LDS-staged p_r, lane h of 2 covers a in [h*KH, h*KH + KH).  On return zc / wc /
+// dsum hold the FULL sums (partner partials added in a commutative, lane-symmetric order).
+template <int K, int TS>
+__device__ __forceinline__ double phase_a_lds(const double* __restrict__ Ps,
+                                              const double* __restrict__ ri,
+                                              const double* __restrict__ rj,
+                                              const double* __restrict__ rk, int h,
+                                              double* __restrict__ crow, double (&zc)[K],
+                                              double (&wc)[K]) {
+  using EP = EPlan<K, TS>;
+  constexpr int KP = EP::KP, KH = EP::KH;
+  constexpr int KE = K & ~1;  // even part of a row (double2 reads)
+  double tj[K], tk[K];
+#pragma unroll
+  for (int g = 0; g < K; ++g) {
+    tj[g] = rj[g];
+    tk[g] = rk[g];
+    zc[g] = 0.0;
+    wc[g] = 0.0;
+  }
+  // p rows are software-pipelined: row (a, b+1) is in flight while row (a, b) is consumed.
+  auto load_row = [&](double (&dst)[K], const double* __restrict__ src) {
+#pragma unroll
+    for (int g = 0; g < KE; g += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(src + g);
+      dst[g] = v.x;
+      dst[g + 1] = v.y;
+    }
+    if constexpr (K & 1) dst[K - 1] = src[K - 1];
+  };
+  // Two p rows per step (two independent U chains for ILP); the next pair is in flight while
+  // the current one is consumed.  Odd K: the last row of a slab pairs with a zero row.
+  constexpr int NPAIR = (K + 1) / 2;
+  double dsum = 0.0;
+  double pv0[K], pv1[K];
+  auto load_pair = [&](double (&d0)[K], double (&d1)[K], const double* __restrict__ slab, int bp) {
+    load_row(d0, slab + (2 * bp) * KP);
+    if (2 * bp + 1 < K) {
+      load_row(d1, slab + (2 * bp + 1) * KP);
+    } else {
+#pragma unroll
+      for (int g = 0; g < K; ++g) d1[g] = 0.0;
+    }
+  };
+  load_pair(pv0, pv1, Ps + EP::slab(h * KH < K ? h * KH : K - 1), 0);
+#pragma unroll 1
+  for (int q = 0; q < KH; ++q) {
+    const int a = h * KH + q;
+    const bool valid = a < K;
+    const int ac = valid ? a : K - 1;
+    const double ta = valid ? ri[ac] : 0.0;
+    const double* __restrict__ pa = Ps + EP::slab(ac);
+    const int an = (a + 1 < K && q + 1 < KH) ? a + 1 : ac;  // next slab (clamped)
+    const double* __restrict__ pn_slab = Ps + EP::slab(an);
+    double y = 0.0;
+#pragma unroll
+    for (int bp = 0; bp < NPAIR; ++bp) {
+      const int b0 = 2 * bp, b1 = 2 * bp + 1;
+      double pn0[K], pn1[K];
+      if (bp + 1 < NPAIR)
+        load_pair(pn0, pn1, pa, bp + 1);
+      else
+        load_pair(pn0, pn1, pn_slab, 0);
+      double u0 = 0.0, u1 = 0.0;
+#pragma unroll
+      for (int g = 0; g < K; ++g) {
+        u0 = fma(pv0[g], tk[g], u0);
+        u1 = fma(pv1[g], tk[g], u1);
+      }
+      const double t0 = ta * tj[b0];
+      y = fma(tj[b0], u0, y);
+      zc[b0] = fma(ta, u0, zc[b0]);
+      if (b1 < K) {
+        const double t1 = ta * tj[b1];
+        y = fma(tj[b1], u1, y);
+        zc[b1] = fma(ta, u1, zc[b1]);
+#pragma unroll
+        for (int g = 0; g < K; ++g) wc[g] = fma(t1, pv1[g], fma(t0, pv0[g], wc[g]));
+      } else {
+#pragma unroll
+        for (int g = 0; g < K; ++g) wc[g] = fma(t0, pv0[g], wc[g]);
+      }
+#pragma unroll
+      for (int g = 0; g < K; ++g) {
+        pv0[g] = pn0[g];
+        pv1[g] = pn1[g];
+      }
+    }
+    if (valid) crow[a] = y;
+    dsum = fma(ta, y, dsum);
+  }
+  // partner exchange (lanes 2l, 2l+1): a + b == b + a exactly, so both lanes agree bitwise
+#pragma unroll
+  for (int g = 0; g < K; ++g) {
+    zc[g] += __shfl_xor(zc[g], 1, 64);
+    wc[g] += __shfl_xor(wc[g], 1, 64);
+  }
+  dsum += __shfl_xor(dsum, 1, 64);
+  return dsum;
+}
+
+// ------------------------------------------------------------------------------------------
+// E-step: grid (n_obs_pad / TS, B), block NT = TS*H.
+// ------------------------------------------------------------------------------------------
+template <int K, int TS>
+__global__ __launch_bounds__((EPlan<K, TS>::NT)) void estep_kernel(
     const int4* __restrict__ obs, const int* __restrict__ tile_r, const double* __restrict__ theta,
     const double* __restrict__ pr, double* __restrict__ contrib, double* __restrict__ cvec,
     double* __restrict__ partS, double* __restrict__ partL, int P, int R, long long n_obs_pad,
     int ntiles, double eps, int ablate) {
-  using T = Tiling<K>;
-  constexpr int K3 = T::K3, KP = T::KP, NB = T::NB, NBC = T::NBC, NBLK = T::NBLK, LG = T::LG,
-                CH = T::CH;
+  using EP = EPlan<K, TS>;
+  using SP = typename EP::S;
+  constexpr int K3 = EP::K3, KP = EP::KP, RS = EP::RS, NT = EP::NT, H = EP::H;
+  constexpr int NB = SP::NB, NBC = SP::NBC, NBLK = SP::NBLK, LG = SP::LG;
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Ps = smem;
+  double* Cs = smem + EP::P_DBL;
+  double* Ri = Cs + EP::CS_DBL;
+  double* Rj = Ri + TS * RS;
+  double* Rk = Rj + TS * RS;
+  double* Cv = Rk + TS * RS;
+  double* scratch = Ri + EP::BODY_DBL;
 
   const int tid = threadIdx.x;
+  const int lo = tid / H;  // observation within the tile
+  const int h = tid % H;   // lane's share of the observation
   const int tile = blockIdx.x;
   const int b = blockIdx.y;
-  const int r = __builtin_amdgcn_readfirstlane(tile_r[tile]);
+  const int r = __builtin_amdgcn_readfirstlane(tile_r[(tile * TS) / TILE]);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-  const size_t o = (size_t)tile * TILE + tid;
+  const size_t o = (size_t)tile * TS + lo;
   const int4 e = obs[o];
   const double n = (double)e.w;
 
-  // ---- phase A
-  double* __restrict__ crow = contrib + ((size_t)b * n_obs_pad + o) * 3 * K;
+  // ---- stage p_r and the observations' theta rows
+  if constexpr (EP::STAGE_P) {
+    for (int idx = tid; idx < K3; idx += NT) {
+      const int a = idx / (K * K);
+      Ps[EP::slab(a) + ((idx / K) % K) * KP + idx % K] = p[idx];
+    }
+  }
+  if (h == 0) {
+    const double* __restrict__ gi = th + (size_t)e.x * K;
+    const double* __restrict__ gj = th + (size_t)e.y * K;
+#pragma unroll
+    for (int g = 0; g < K; ++g) {
+      Ri[lo * RS + g] = gi[g];
+      Rj[lo * RS + g] = gj[g];
+    }
+  }
+  if (h == H - 1) {
+    const double* __restrict__ gk = th + (size_t)e.z * K;
+#pragma unroll
+    for (int g = 0; g < K; ++g) Rk[lo * RS + g] = gk[g];
+  }
+  __syncthreads();
+
+  // ---- phase A (LDS path: Y/Z/W rows staged in Cs, written out as one contiguous block)
+  double* __restrict__ crow =
+      EP::STAGE_P ? Cs + lo * 3 * K : contrib + ((size_t)b * n_obs_pad + o) * 3 * K;
+  double dsum = 1.0;
   // ablate (measurement builds only, MMSBM_ABLATE): bit 0 skips phase A, bit 1 phase B
-  const double d = ((ablate & 1) ? 1.0 : phase_a<K>(th, p, e, crow)) + eps;
+  if (!(ablate & 1)) {
+    if constexpr (EP::STAGE_P) {
+      double zc[K], wc[K];
+      dsum = phase_a_lds<K, TS>(Ps, Ri + lo * RS, Rj + lo * RS, Rk + lo * RS, h, crow, zc, wc);
+      if (h == 0) {
+#pragma unroll
+        for (int g = 0; g < K; ++g) crow[K + g] = zc[g];
+      } else {
+#pragma unroll
+        for (int g = 0; g < K; ++g) crow[2 * K + g] = wc[g];
+      }
+    } else {
+      dsum = phase_a<K>(th, p, e, crow);
+    }
+  }
+  const double d = dsum + eps;
   const double c = n / d;
-  cvec[(size_t)b * n_obs_pad + o] = c;
-  const double ll = block_sum(n * log(d), smem);
+  if (h == 0) {
+    cvec[(size_t)b * n_obs_pad + o] = c;
+    Cv[lo] = c;
+  }
+  const double ll = block_sum(h == 0 ? n * log(d) : 0.0, scratch);  // barrier for phase B
   if (tid == 0) partL[(size_t)b * ntiles + tile] = ll;
+  if constexpr (EP::STAGE_P) {
+    // the tile's TS contrib rows are one contiguous block: coalesced 16-B stores
+    double2* __restrict__ dst =
+        reinterpret_cast<double2*>(contrib + ((size_t)b * n_obs_pad + (size_t)tile * TS) * 3 * K);
+    const double2* src = reinterpret_cast<const double2*>(Cs);
+    if (!(ablate & 4))
+      for (int idx = tid; idx < TS * 3 * K / 2; idx += NT) dst[idx] = src[idx];
+  }
 
   // ---- phase B: S_r[a b g] = sum_l c_l th_i[a] th_j[b] th_k[g] over this tile
-  double* As = smem;
-  double* Bs = smem + CH * KP;
-  double* Gs = smem + 2 * CH * KP;
   double* __restrict__ sdst = partS + ((size_t)b * ntiles + tile) * K3;
-  for (int set = 0; set < ((ablate & 2) ? 0 : T::NSETS); ++set) {
+  for (int set = 0; set < ((ablate & 2) ? 0 : SP::NSETS); ++set) {
     int blk, grp;
-    if constexpr (T::NSETS == 1) {
+    if constexpr (SP::NSETS == 1) {
       blk = tid % NBLK;
       grp = tid / NBLK;
     } else {
-      blk = set * TILE + tid;
+      blk = set * NT + tid;
       grp = 0;
     }
     const bool active = (grp < LG) && (blk < NBLK);
@@ -301,42 +492,30 @@ __global__ __launch_bounds__(TILE) void estep_kernel(
     for (int q = 0; q < NB; ++q)
 #pragma unroll
       for (int g = 0; g < K; ++g) acc[q][g] = 0.0;
-
-    for (int ch = 0; ch < TILE / CH; ++ch) {
-      __syncthreads();
-      if (tid / CH == ch) {
-        const int l = tid % CH;
-        const double* __restrict__ ri = th + (size_t)e.x * K;
-        const double* __restrict__ rj = th + (size_t)e.y * K;
-        const double* __restrict__ rk = th + (size_t)e.z * K;
-#pragma unroll
-        for (int g = 0; g < K; ++g) {
-          As[l * KP + g] = c * ri[g];
-          Bs[l * KP + g] = rj[g];
-          Gs[l * KP + g] = rk[g];
-        }
-      }
-      __syncthreads();
-      if (active) {
+    if (active) {
 #pragma unroll 2
-        for (int l = grp; l < CH; l += LG) {
-          const double av = As[l * KP + alpha];
-          double gv[K];
+      for (int l = grp; l < TS; l += LG) {
+        const double av = Cv[l] * Ri[l * RS + alpha];
+        double gv[K];
 #pragma unroll
-          for (int g = 0; g < K; ++g) gv[g] = Gs[l * KP + g];
+        for (int g = 0; g < (K & ~1); g += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(Rk + l * RS + g);
+          gv[g] = v.x;
+          gv[g + 1] = v.y;
+        }
+        if constexpr (K & 1) gv[K - 1] = Rk[l * RS + K - 1];
 #pragma unroll
-          for (int q = 0; q < NB; ++q) {
-            if (NB * NBC == K || beta0 + q < K) {
-              const double ab = av * Bs[l * KP + beta0 + q];
+        for (int q = 0; q < NB; ++q) {
+          if (NB * NBC == K || beta0 + q < K) {
+            const double ab = av * Rj[l * RS + beta0 + q];
 #pragma unroll
-              for (int g = 0; g < K; ++g) acc[q][g] = fma(ab, gv[g], acc[q][g]);
-            }
+            for (int g = 0; g < K; ++g) acc[q][g] = fma(ab, gv[g], acc[q][g]);
           }
         }
       }
     }
     if constexpr (LG > 1) {
-      double* red = smem;
+      double* red = Ri;  // rows are dead once every group has accumulated
       int ng = LG;
       while (ng > 1) {
         const int half = (ng + 1) / 2;
@@ -561,6 +740,7 @@ struct mmsbm_ctx {
   // optional per-kernel timing: HIP event pairs recorded around each launch on its stream
   bool timing = false;
   int ablate = 0;  // MMSBM_ABLATE (measurement only)
+  int ts = 64;     // E-step tile (observations per workgroup): MMSBM_ESTEP_TILE = 64/128/256
   std::vector<hipEvent_t> ev[2];  // start/stop pairs per kernel id
   size_t nev[2] = {0, 0};
 };
@@ -581,38 +761,66 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   off += align_up((size_t)c->B * tr.n_obs_pad * 3 * c->K * sizeof(double));
   L.cvec = off;
   off += align_up((size_t)c->B * tr.n_obs_pad * sizeof(double));
-  L.partS = off;
-  off += align_up((size_t)c->B * tr.ntiles * K3 * sizeof(double));
+  L.partS = off;  // one row per E-step tile; sized for the smallest tile (MIN_TS)
+  const long long et = tr.n_obs_pad / MIN_TS;
+  off += align_up((size_t)c->B * et * K3 * sizeof(double));
   L.partL = off;
-  const int nt = tr.ntiles > te.ntiles ? tr.ntiles : te.ntiles;
+  long long nt = et > te.ntiles ? et : te.ntiles;
   off += align_up((size_t)c->B * (nt > 0 ? nt : 1) * sizeof(double));
   L.total = off;
   return L;
 }
 
+// E-step tile actually used for a requested one: the largest that fits the LDS plan.
 template <int K>
-int launch_estep(mmsbm_ctx* c, const double*, const double*, hipStream_t s) {
-  using T = Tiling<K>;
+int estep_tile(int requested) {
+  if (requested >= 256 && EPlan<K, 256>::FITS) return 256;
+  if (requested >= 128 && EPlan<K, 128>::FITS) return 128;
+  return 64;
+}
+
+template <int K, int TS>
+int launch_estep_ts(mmsbm_ctx* c, hipStream_t s) {
+  using T = EPlan<K, TS>;
+  static_assert(T::FITS, "E-step LDS plan over budget");
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
-  if (tr.ntiles == 0) return MMSBM_OK;
-  estep_kernel<K><<<dim3(tr.ntiles, c->B), TILE, T::LDS_BYTES, s>>>(
+  const int et = (int)(tr.n_obs_pad / TS);
+  estep_kernel<K, TS><<<dim3(et, c->B), T::NT, T::LDS_BYTES, s>>>(
       tr.obs, tr.tile_r, c->theta_mut, c->pr_mut, c->contrib, c->cvec, c->partS, c->partL, c->P,
-      c->R, tr.n_obs_pad, tr.ntiles, c->eps, c->ablate);
+      c->R, tr.n_obs_pad, et, c->eps, c->ablate);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
+}
+
+template <int K>
+int launch_estep(mmsbm_ctx* c, const double*, const double*, hipStream_t s) {
+  const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
+  if (tr.ntiles == 0) return MMSBM_OK;
+  switch (estep_tile<K>(c->ts)) {
+    case 256:
+      if constexpr (EPlan<K, 256>::FITS) return launch_estep_ts<K, 256>(c, s);
+      break;
+    case 128:
+      if constexpr (EPlan<K, 128>::FITS) return launch_estep_ts<K, 128>(c, s);
+      break;
+    default:
+      break;
+  }
+  return launch_estep_ts<K, 64>(c, s);
 }
 
 template <int K>
 int launch_mstep(mmsbm_ctx* c, hipStream_t s) {
   constexpr int K3 = K * K * K;
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
-  Segs segs{};
-  for (int r = 0; r <= c->R; ++r) segs.t[r] = (int)(tr.seg.empty() ? 0 : tr.seg[r] / TILE);
+  const int ts = estep_tile<K>(c->ts);
+  Segs segs{};  // rating groups in units of E-step tiles
+  for (int r = 0; r <= c->R; ++r) segs.t[r] = (int)(tr.seg.empty() ? 0 : tr.seg[r] / ts);
   const int theta_blocks = (c->P + 3) / 4;
   const int p_blocks = (K3 + MP_CELLS - 1) / MP_CELLS;
   mstep_kernel<K><<<dim3(theta_blocks + p_blocks, c->B), 256, 0, s>>>(
       c->theta_mut, c->pr_mut, c->contrib, c->cvec, c->gptr, c->ginc, c->deg, c->partS, segs,
-      c->P, c->R, tr.ntiles, tr.n_obs_pad, theta_blocks, c->eps);
+      c->P, c->R, (int)(tr.n_obs_pad / ts), tr.n_obs_pad, theta_blocks, c->eps);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -682,6 +890,10 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   auto* c = new mmsbm_ctx();
   c->device = device;
   if (const char* ab = getenv("MMSBM_ABLATE")) c->ablate = atoi(ab);
+  if (const char* t = getenv("MMSBM_ESTEP_TILE")) {
+    const int v = atoi(t);
+    if (v == 64 || v == 128 || v == 256) c->ts = v;
+  }
   *out = c;
   return MMSBM_OK;
 }
