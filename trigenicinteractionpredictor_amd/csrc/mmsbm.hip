@@ -555,18 +555,21 @@ struct Segs {
   int t[MAX_R + 1];  // tile offsets of each rating group
 };
 
-constexpr int MP_CELLS = 16;  // p M-step: cells per block
-constexpr int MP_PARTS = 16;  // p M-step: tile stripes per cell
+constexpr int MP_CELLS = 4;   // p M-step: cells per block
+constexpr int MP_PARTS = 64;  // p M-step: tile stripes per cell
+constexpr int MT_BATCH = 4;   // theta M-step: incidences in flight per lane
 
 // ------------------------------------------------------------------------------------------
 // Fused M-step, grid (theta_blocks + ceil(K3 / MP_CELLS), B), block 256.
 //  blocks [0, theta_blocks): theta (:1016-1018), one wave per gene:
 //      theta[g][a] <- theta[g][a] * (sum over the gene's incidences of c * row[a]) / deg[g]
-//    lanes stride the incidence list, each keeps K partial sums, then a fixed butterfly.
-//  blocks [theta_blocks, ...): p (:1021-1028), 16 cells x 16 tile stripes per block:
+//    lanes stride the incidence list MT_BATCH entries at a time (all loads of a batch in
+//    flight together), each keeps K partial sums, then a fixed butterfly.
+//  blocks [theta_blocks, ...): p (:1021-1028), MP_CELLS cells x MP_PARTS tile stripes:
 //      S_r = sum of the per-tile partials of rating r; npr_r = p_r S_r;
 //      p_r <- npr_r / (eps + sum_r npr_r).
 // Both halves read only E-step outputs and write disjoint parameters, so they share a launch.
+// Every sum has a fixed order (bitwise reproducible).
 // ------------------------------------------------------------------------------------------
 template <int K>
 __global__ __launch_bounds__(256) void mstep_kernel(
@@ -585,13 +588,27 @@ __global__ __launch_bounds__(256) void mstep_kernel(
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    const int q1 = gptr[g + 1];
-    for (int q = gptr[g] + lane; q < q1; q += 64) {
-      const int inc = ginc[q];
-      const double c = cv[inc / 3];
-      const double* __restrict__ row = cb + (size_t)inc * K;
+    const int q0 = gptr[g], q1 = gptr[g + 1];
+    for (int qb = q0; qb < q1; qb += 64 * MT_BATCH) {
+      int inc[MT_BATCH];
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc[k] = fma(c, row[k], acc[k]);
+      for (int j = 0; j < MT_BATCH; ++j) {
+        const int q = qb + j * 64 + lane;
+        inc[j] = q < q1 ? ginc[q] : -1;
+      }
+      double cc[MT_BATCH], row[MT_BATCH][K];
+#pragma unroll
+      for (int j = 0; j < MT_BATCH; ++j) {
+        const int ij = inc[j] < 0 ? 0 : inc[j];
+        cc[j] = inc[j] < 0 ? 0.0 : cv[ij / 3];
+        const double* __restrict__ src = cb + (size_t)ij * K;
+#pragma unroll
+        for (int k = 0; k < K; ++k) row[j][k] = src[k];
+      }
+#pragma unroll
+      for (int j = 0; j < MT_BATCH; ++j)
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] = fma(cc[j], row[j][k], acc[k]);
     }
     double mine = 0.0;
 #pragma unroll
@@ -600,8 +617,8 @@ __global__ __launch_bounds__(256) void mstep_kernel(
       if (lane == k) mine = t;
     }
     if (lane < K) {
-      double* row = theta + (size_t)b * P * K + (size_t)g * K;
-      row[lane] = row[lane] * mine / (double)deg[g];
+      double* th = theta + (size_t)b * P * K + (size_t)g * K;
+      th[lane] = th[lane] * mine / (double)deg[g];
     }
     return;
   }
