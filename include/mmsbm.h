@@ -75,7 +75,10 @@ int mmsbm_set_shape(mmsbm_ctx *ctx, int32_t K, int32_t R, int32_t B, int32_t P, 
 int mmsbm_set_links(mmsbm_ctx *ctx, int32_t which, const int32_t *obs, int64_t n_obs_pad,
                     const int64_t *seg_host);
 
-/* Gene incidence CSR of the TRAIN set for the theta M-step (:1016-1018).
+/* Gene incidence CSR of the TRAIN set for the theta M-step (:1016-1018).  Call after
+ * mmsbm_set_links(MMSBM_SET_TRAIN) (re-setting the train links requires calling it again).
+ * The engine inverts it once on the device: every observation's three responsibility rows
+ * are then written straight to their gene's contiguous CSR run.
  * Validates deg > 0 for every gene (copies deg to the host once); a zero
  * returns MMSBM_ERR_ZERO_DEGREE and makes mmsbm_iterate fail the same way. */
 int mmsbm_set_genes(mmsbm_ctx *ctx, const int32_t *gene_ptr, const int32_t *gene_inc,
@@ -100,11 +103,12 @@ int mmsbm_loglik(mmsbm_ctx *ctx, int32_t which, const double *theta, const doubl
 int mmsbm_predict(mmsbm_ctx *ctx, const int32_t *ids, int64_t n, const double *theta,
                   const double *pr, double *out, void *stream);
 
-/* Kernel timing for measurement (bench.py): while enabled, mmsbm_iterate records a HIP event
- * pair on the launch stream around every kernel (ids: 0 E-step, 1 M-step).
+/* Kernel timing for measurement (bench.py): with stride n > 0, mmsbm_iterate records a HIP
+ * event pair on the launch stream around every kernel of every n-th iteration (kernel ids:
+ * 0 E-step, 1 M1 = S accumulation + theta gather, 2 M2 = p update); 0 disables.
  * mmsbm_timing resets the counters; mmsbm_timing_result waits for the last event and returns
- * the summed device time (ms) and the number of launches of that kernel. */
-int mmsbm_timing(mmsbm_ctx *ctx, int32_t enable);
+ * the summed device time (ms) and the number of timed launches of that kernel. */
+int mmsbm_timing(mmsbm_ctx *ctx, int32_t stride);
 int mmsbm_timing_result(mmsbm_ctx *ctx, int32_t kernel, double *total_ms, int64_t *count);
 
 #ifdef __cplusplus

@@ -1,7 +1,7 @@
 // mmsbm.hip — MI355X (gfx950) MMSBM EM engine: kernels + C ABI (include/mmsbm.h).
 //
 // Hot path of AleixMT/TrigenicInteractionPredictor, src/TrigenicInteractionPredictor.py:
-//   make_iteration      :984-1043   -> estep_kernel + mstep_kernel (theta and p halves)
+//   make_iteration      :984-1043   -> estep_kernel, m1_kernel (S, theta gather), m2_kernel (p)
 //   compute_likelihood  :952-974    -> loglik_kernel + reduce_kernel
 //   do_prediction       :530-547    -> predict_kernel
 //
@@ -50,7 +50,8 @@ namespace {
 constexpr int TILE = MMSBM_TILE;
 constexpr int MAX_R = 8;
 constexpr int LDS_BUDGET = 64 * 1024;
-constexpr int MIN_TS = 64;  // smallest E-step tile (observations per workgroup)
+constexpr int SACC_WGS = 256;      // default S-accumulation workgroups (MMSBM_SACC_WGS)
+constexpr int SACC_WGS_MAX = 2048;
 
 thread_local std::string g_err;
 
@@ -74,8 +75,9 @@ int fail(int code, const char* fmt, ...) {
 // Compile-time tiling of the S accumulation (phase B) for a given K.
 // ------------------------------------------------------------------------------------------
 constexpr int pick_nb(int K) {
-  // cells per lane = NB * K <= 64 doubles; prefer a divisor of K (no ragged b-chunk).
-  int cap = 64 / K;
+  // cells per lane = NB * K <= 50 doubles (fits 3 waves/SIMD with phase A's live set);
+  // prefer a divisor of K (no ragged b-chunk).
+  int cap = 50 / K;
   if (cap < 1) cap = 1;
   if (cap > K) cap = K;
   int best = 1;
@@ -120,11 +122,12 @@ __device__ __forceinline__ double block_sum(double v, double* scratch) {
 
 // ------------------------------------------------------------------------------------------
 // Phase A: per-observation contractions.  One lane = one observation.  p_r is wave-uniform.
-// Returns sum_a th_i[a] Y[a]; stores Y, Z, W (unscaled) into crow[0:K], [K:2K], [2K:3K].
+// Returns sum_a th_i[a] Y[a]; stores Y, Z, W (unscaled) into the rows ry, rz, rw.
 // ------------------------------------------------------------------------------------------
 template <int K>
 __device__ __forceinline__ double phase_a(const double* __restrict__ th, const double* __restrict__ p,
-                                          const int4 e, double* __restrict__ crow) {
+                                          const int4 e, double* __restrict__ ry,
+                                          double* __restrict__ rz, double* __restrict__ rw) {
   constexpr int K2 = K * K;
   const double* __restrict__ ri = th + (size_t)e.x * K;
   const double* __restrict__ rj = th + (size_t)e.y * K;
@@ -160,13 +163,13 @@ __device__ __forceinline__ double phase_a(const double* __restrict__ th, const d
 #pragma unroll
         for (int g = 0; g < K; ++g) wc[g] = fma(t, pa[b * K + g], wc[g]);
       }
-      crow[a] = y;
+      ry[a] = y;
       dsum = fma(ta, y, dsum);
     }
 #pragma unroll
     for (int g = 0; g < K; ++g) {
-      crow[K + g] = zc[g];
-      crow[2 * K + g] = wc[g];
+      rz[g] = zc[g];
+      rw[g] = wc[g];
     }
   } else {
     // two passes keep the live set at 3K (pass 1) / 2K (pass 2) doubles
@@ -185,11 +188,11 @@ __device__ __forceinline__ double phase_a(const double* __restrict__ th, const d
         y = fma(tj[b], u, y);
         zc[b] = fma(ta, u, zc[b]);
       }
-      crow[a] = y;
+      ry[a] = y;
       dsum = fma(ta, y, dsum);
     }
 #pragma unroll
-    for (int g = 0; g < K; ++g) crow[K + g] = zc[g];
+    for (int g = 0; g < K; ++g) rz[g] = zc[g];
     double wc[K];
 #pragma unroll
     for (int g = 0; g < K; ++g) wc[g] = 0.0;
@@ -207,7 +210,7 @@ __device__ __forceinline__ double phase_a(const double* __restrict__ th, const d
       }
     }
 #pragma unroll
-    for (int g = 0; g < K; ++g) crow[2 * K + g] = wc[g];
+    for (int g = 0; g < K; ++g) rw[g] = wc[g];
   }
   return dsum;
 }
@@ -247,50 +250,67 @@ __device__ __forceinline__ double contract(const double* __restrict__ th, const 
 }
 
 // ------------------------------------------------------------------------------------------
-// E-step plan.  TS observations per workgroup, H lanes per observation (NT = TS*H threads).
-//   K <= 12: p_r is staged in LDS once per workgroup and read with ds_read_b128 (broadcast);
-//            H = 2: the two lanes of an observation split the a-range and exchange their
-//            Z / W / d partials with one lane swap (2x the waves of one-lane-per-observation:
-//            a fold0-sized problem otherwise leaves ~1 wave per SIMD to hide all latency).
-//   K > 12:  p_r streams through the scalar cache (SGPR operands), H = 1.
-// LDS: Ps [K slabs of K*KP, second half shifted by 16 B so the two lanes' reads hit distinct
-//      banks], Ri/Rj/Rk [TS][RS] theta rows of every observation (RS = 2 mod 4 doubles:
-//      conflict-free 16-lane ds_read_b128), Cv [TS] c = n/d, red (phase-B reduction, aliases
-//      the rows once accumulation is done), 8 doubles of block-sum scratch.
+// E-step plan.  ET = 64 observations per workgroup, H lanes per observation (NT = 64*H).
+//   K in {1..8, 10, 12}: p_r is staged in LDS once per workgroup and read with wave-uniform
+//            ds_read_b128 (broadcast, conflict-free); H = 2: the two lanes of an observation
+//            split the a-range and exchange their Z / W / d partials with one lane swap (twice
+//            the waves of one lane per observation: a fold0-sized problem otherwise leaves ~1
+//            wave per SIMD to hide every latency).
+//   other K: p_r streams through the scalar cache (SGPR operands), H = 1.
+// LDS: Ps = K slabs of K*KP doubles, the second half shifted by 16 B so that the two lanes'
+//      reads of one instruction hit distinct banks; 8 doubles of block-sum scratch.
 // ------------------------------------------------------------------------------------------
-template <int K, int TS>
+constexpr int ET = 64;
+
+template <int K>
 struct EPlan {
-  static constexpr bool STAGE_P = K <= 12;
+  static constexpr bool STAGE_P = K <= 12 && K != 9 && K != 11;
   static constexpr int H = STAGE_P ? 2 : 1;
-  static constexpr int NT = TS * H;
-  using S = SPlan<K, NT>;
+  static constexpr int NT = ET * H;
   static constexpr int K3 = K * K * K;
   static constexpr int KP = (K + 1) & ~1;
-  static constexpr int KH = (K + H - 1) / H;   // a-range per lane
-  static constexpr int RS = (KP % 4 == 2) ? KP : KP + 2;
+  static constexpr int KH = (K + H - 1) / H;  // a-range per lane
   static constexpr int P_DBL = STAGE_P ? K * K * KP + 2 : 0;
-  static constexpr int CS_DBL = STAGE_P ? TS * 3 * K : 0;  // contrib rows, written out coalesced
-  static constexpr int ROWS_DBL = 3 * TS * RS;
-  static constexpr int RED_DBL = (S::LG / 2) * K3;
-  static constexpr int BODY_DBL = ROWS_DBL + TS > RED_DBL ? ROWS_DBL + TS : RED_DBL;
-  static constexpr int LDS_BYTES = (P_DBL + CS_DBL + BODY_DBL + 8) * 8;
-  static constexpr bool FITS = LDS_BYTES <= LDS_BUDGET;
+  static constexpr int LDS_BYTES = (P_DBL + 8) * 8;
+  // waves/SIMD the register allocator must leave room for (3 keeps a fold0 grid resident)
+  static constexpr int OCC = STAGE_P ? 3 : 1;
   __device__ static constexpr int slab(int a) { return a * K * KP + (a >= KH ? 2 : 0); }
 };
 
-// Phase A, LDS-staged p_r, lane h of 2 covers a in [h*KH, h*KH + KH).  On return zc / wc /
-// dsum hold the FULL sums (partner partials added in a commutative, lane-symmetric order).
-template <int K, int TS>
+template <int K>
+__device__ __forceinline__ void stage_p(double* __restrict__ Ps, const double* __restrict__ p,
+                                        int tid, int nt) {
+  using EP = EPlan<K>;
+  for (int idx = tid; idx < EP::K3; idx += nt) {
+    const int a = idx / (K * K);
+    Ps[EP::slab(a) + ((idx / K) % K) * EP::KP + idx % K] = p[idx];
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void lds_row(double (&dst)[K], const double* __restrict__ src) {
+#pragma unroll
+  for (int g = 0; g < (K & ~1); g += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(src + g);
+    dst[g] = v.x;
+    dst[g + 1] = v.y;
+  }
+  if constexpr (K & 1) dst[K - 1] = src[K - 1];
+}
+
+// Phase A with p_r in LDS, lane h of 2 covering a in [h*KH, h*KH + KH).  Returns Y[a] of its
+// own a-range in yv; on return zc / wc / dsum hold the FULL sums (partner partials added
+// in a commutative, lane-symmetric order, so both lanes agree bitwise).
+template <int K>
 __device__ __forceinline__ double phase_a_lds(const double* __restrict__ Ps,
                                               const double* __restrict__ ri,
                                               const double* __restrict__ rj,
                                               const double* __restrict__ rk, int h,
-                                              double* __restrict__ crow, double (&zc)[K],
+                                              double (&yv)[EPlan<K>::KH], double (&zc)[K],
                                               double (&wc)[K]) {
-  using EP = EPlan<K, TS>;
-  constexpr int KP = EP::KP, KH = EP::KH;
-  constexpr int KE = K & ~1;  // even part of a row (double2 reads)
-  double tj[K], tk[K];
+  using EP = EPlan<K>;
+  constexpr int KP = EP::KP, KH = EP::KH, NPAIR = (K + 1) / 2;
+  double tj[K], tk[K], ti[KH];
 #pragma unroll
   for (int g = 0; g < K; ++g) {
     tj[g] = rj[g];
@@ -298,49 +318,28 @@ __device__ __forceinline__ double phase_a_lds(const double* __restrict__ Ps,
     zc[g] = 0.0;
     wc[g] = 0.0;
   }
-  // p rows are software-pipelined: row (a, b+1) is in flight while row (a, b) is consumed.
-  auto load_row = [&](double (&dst)[K], const double* __restrict__ src) {
 #pragma unroll
-    for (int g = 0; g < KE; g += 2) {
-      const double2 v = *reinterpret_cast<const double2*>(src + g);
-      dst[g] = v.x;
-      dst[g + 1] = v.y;
-    }
-    if constexpr (K & 1) dst[K - 1] = src[K - 1];
-  };
-  // Two p rows per step (two independent U chains for ILP); the next pair is in flight while
-  // the current one is consumed.  Odd K: the last row of a slab pairs with a zero row.
-  constexpr int NPAIR = (K + 1) / 2;
+  for (int q = 0; q < KH; ++q) ti[q] = (h * KH + q < K) ? ri[h * KH + q] : 0.0;
   double dsum = 0.0;
-  double pv0[K], pv1[K];
-  auto load_pair = [&](double (&d0)[K], double (&d1)[K], const double* __restrict__ slab, int bp) {
-    load_row(d0, slab + (2 * bp) * KP);
-    if (2 * bp + 1 < K) {
-      load_row(d1, slab + (2 * bp + 1) * KP);
-    } else {
+  // Two p rows per step: two independent U chains for ILP.
 #pragma unroll
-      for (int g = 0; g < K; ++g) d1[g] = 0.0;
-    }
-  };
-  load_pair(pv0, pv1, Ps + EP::slab(h * KH < K ? h * KH : K - 1), 0);
-#pragma unroll 1
   for (int q = 0; q < KH; ++q) {
     const int a = h * KH + q;
     const bool valid = a < K;
-    const int ac = valid ? a : K - 1;
-    const double ta = valid ? ri[ac] : 0.0;
-    const double* __restrict__ pa = Ps + EP::slab(ac);
-    const int an = (a + 1 < K && q + 1 < KH) ? a + 1 : ac;  // next slab (clamped)
-    const double* __restrict__ pn_slab = Ps + EP::slab(an);
+    const double ta = ti[q];
+    const double* __restrict__ pa = Ps + EP::slab(valid ? a : K - 1);
     double y = 0.0;
 #pragma unroll
     for (int bp = 0; bp < NPAIR; ++bp) {
       const int b0 = 2 * bp, b1 = 2 * bp + 1;
-      double pn0[K], pn1[K];
-      if (bp + 1 < NPAIR)
-        load_pair(pn0, pn1, pa, bp + 1);
-      else
-        load_pair(pn0, pn1, pn_slab, 0);
+      double pv0[K], pv1[K];
+      lds_row<K>(pv0, pa + b0 * KP);
+      if (b1 < K) {
+        lds_row<K>(pv1, pa + b1 * KP);
+      } else {
+#pragma unroll
+        for (int g = 0; g < K; ++g) pv1[g] = 0.0;
+      }
       double u0 = 0.0, u1 = 0.0;
 #pragma unroll
       for (int g = 0; g < K; ++g) {
@@ -360,16 +359,10 @@ __device__ __forceinline__ double phase_a_lds(const double* __restrict__ Ps,
 #pragma unroll
         for (int g = 0; g < K; ++g) wc[g] = fma(t0, pv0[g], wc[g]);
       }
-#pragma unroll
-      for (int g = 0; g < K; ++g) {
-        pv0[g] = pn0[g];
-        pv1[g] = pn1[g];
-      }
     }
-    if (valid) crow[a] = y;
+    yv[q] = y;
     dsum = fma(ta, y, dsum);
   }
-  // partner exchange (lanes 2l, 2l+1): a + b == b + a exactly, so both lanes agree bitwise
 #pragma unroll
   for (int g = 0; g < K; ++g) {
     zc[g] += __shfl_xor(zc[g], 1, 64);
@@ -380,108 +373,184 @@ __device__ __forceinline__ double phase_a_lds(const double* __restrict__ Ps,
 }
 
 // ------------------------------------------------------------------------------------------
-// E-step: grid (n_obs_pad / TS, B), block NT = TS*H.
+// E-step (phase A of :987-1012): grid (n_obs_pad / ET, B), block NT.
+//   The three c-scaled contribution rows of an observation, c*Y -> ntheta[i], c*Z -> ntheta[j],
+//   c*W -> ntheta[k], are stored at the observation's positions in the gene incidence CSR
+//   (pos[o] = (q0, q1, q2)), so that M1 reads every gene's rows as one contiguous run.
+//   cvec[b][o] <- c = n / d;  partL[b][tile] <- sum n log d (likelihood of the incoming
+//   parameters, for free).
 // ------------------------------------------------------------------------------------------
-template <int K, int TS>
-__global__ __launch_bounds__((EPlan<K, TS>::NT)) void estep_kernel(
-    const int4* __restrict__ obs, const int* __restrict__ tile_r, const double* __restrict__ theta,
-    const double* __restrict__ pr, double* __restrict__ contrib, double* __restrict__ cvec,
-    double* __restrict__ partS, double* __restrict__ partL, int P, int R, long long n_obs_pad,
-    int ntiles, double eps, int ablate) {
-  using EP = EPlan<K, TS>;
-  using SP = typename EP::S;
-  constexpr int K3 = EP::K3, KP = EP::KP, RS = EP::RS, NT = EP::NT, H = EP::H;
-  constexpr int NB = SP::NB, NBC = SP::NBC, NBLK = SP::NBLK, LG = SP::LG;
+template <int K>
+__global__ __launch_bounds__((EPlan<K>::NT), (EPlan<K>::OCC)) void estep_kernel(
+    const int4* __restrict__ obs, const int4* __restrict__ pos, const int* __restrict__ tile_r,
+    const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ contrib,
+    double* __restrict__ cvec, double* __restrict__ partL, int P, int R, long long n_obs_pad,
+    long long nnz, int ntiles, double eps, int ablate) {
+  using EP = EPlan<K>;
+  constexpr int K3 = EP::K3, H = EP::H, NT = EP::NT, KH = EP::KH;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* Ps = smem;
-  double* Cs = smem + EP::P_DBL;
-  double* Ri = Cs + EP::CS_DBL;
-  double* Rj = Ri + TS * RS;
-  double* Rk = Rj + TS * RS;
-  double* Cv = Rk + TS * RS;
-  double* scratch = Ri + EP::BODY_DBL;
+  double* scratch = smem + EP::P_DBL;
 
   const int tid = threadIdx.x;
   const int lo = tid / H;  // observation within the tile
   const int h = tid % H;   // lane's share of the observation
   const int tile = blockIdx.x;
   const int b = blockIdx.y;
-  const int r = __builtin_amdgcn_readfirstlane(tile_r[(tile * TS) / TILE]);
+  const int r = __builtin_amdgcn_readfirstlane(tile_r[(tile * ET) / TILE]);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-  const size_t o = (size_t)tile * TS + lo;
+  const size_t o = (size_t)tile * ET + lo;
   const int4 e = obs[o];
+  const int4 q = pos[o];  // CSR rows of slots 0, 1, 2 (-1 for padding)
   const double n = (double)e.w;
-
-  // ---- stage p_r and the observations' theta rows
+  double* __restrict__ cb = contrib + (size_t)b * nnz * K;
   if constexpr (EP::STAGE_P) {
-    for (int idx = tid; idx < K3; idx += NT) {
-      const int a = idx / (K * K);
-      Ps[EP::slab(a) + ((idx / K) % K) * KP + idx % K] = p[idx];
-    }
+    stage_p<K>(Ps, p, tid, NT);
+    __syncthreads();
   }
-  if (h == 0) {
-    const double* __restrict__ gi = th + (size_t)e.x * K;
-    const double* __restrict__ gj = th + (size_t)e.y * K;
-#pragma unroll
-    for (int g = 0; g < K; ++g) {
-      Ri[lo * RS + g] = gi[g];
-      Rj[lo * RS + g] = gj[g];
-    }
-  }
-  if (h == H - 1) {
-    const double* __restrict__ gk = th + (size_t)e.z * K;
-#pragma unroll
-    for (int g = 0; g < K; ++g) Rk[lo * RS + g] = gk[g];
-  }
-  __syncthreads();
-
-  // ---- phase A (LDS path: Y/Z/W rows staged in Cs, written out as one contiguous block)
-  double* __restrict__ crow =
-      EP::STAGE_P ? Cs + lo * 3 * K : contrib + ((size_t)b * n_obs_pad + o) * 3 * K;
   double dsum = 1.0;
-  // ablate (measurement builds only, MMSBM_ABLATE): bit 0 skips phase A, bit 1 phase B
-  if (!(ablate & 1)) {
-    if constexpr (EP::STAGE_P) {
-      double zc[K], wc[K];
-      dsum = phase_a_lds<K, TS>(Ps, Ri + lo * RS, Rj + lo * RS, Rk + lo * RS, h, crow, zc, wc);
-      if (h == 0) {
-#pragma unroll
-        for (int g = 0; g < K; ++g) crow[K + g] = zc[g];
-      } else {
-#pragma unroll
-        for (int g = 0; g < K; ++g) crow[2 * K + g] = wc[g];
-      }
-    } else {
-      dsum = phase_a<K>(th, p, e, crow);
-    }
-  }
-  const double d = dsum + eps;
-  const double c = n / d;
-  if (h == 0) {
-    cvec[(size_t)b * n_obs_pad + o] = c;
-    Cv[lo] = c;
-  }
-  const double ll = block_sum(h == 0 ? n * log(d) : 0.0, scratch);  // barrier for phase B
-  if (tid == 0) partL[(size_t)b * ntiles + tile] = ll;
+  // ablate (measurement builds only, MMSBM_ABLATE): bit 0 skips phase A
   if constexpr (EP::STAGE_P) {
-    // the tile's TS contrib rows are one contiguous block: coalesced 16-B stores
-    double2* __restrict__ dst =
-        reinterpret_cast<double2*>(contrib + ((size_t)b * n_obs_pad + (size_t)tile * TS) * 3 * K);
-    const double2* src = reinterpret_cast<const double2*>(Cs);
-    if (!(ablate & 4))
-      for (int idx = tid; idx < TS * 3 * K / 2; idx += NT) dst[idx] = src[idx];
+    double yv[KH], zc[K], wc[K];
+    if (!(ablate & 1))
+      dsum = phase_a_lds<K>(Ps, th + (size_t)e.x * K, th + (size_t)e.y * K, th + (size_t)e.z * K,
+                            h, yv, zc, wc);
+    const double d = dsum + eps;
+    const double c = n / d;
+    if (q.x >= 0 && !(ablate & 1)) {
+      double* ry = cb + (size_t)q.x * K + h * KH;
+#pragma unroll
+      for (int t = 0; t < KH; ++t)
+        if (h * KH + t < K) ry[t] = c * yv[t];
+      double* rzw = cb + (size_t)(h == 0 ? q.y : q.z) * K;
+#pragma unroll
+      for (int g = 0; g < K; ++g) rzw[g] = c * (h == 0 ? zc[g] : wc[g]);
+    }
+    if (h == 0) cvec[(size_t)b * n_obs_pad + o] = c;
+    const double ll = block_sum(h == 0 ? n * log(d) : 0.0, scratch);
+    if (tid == 0) partL[(size_t)b * ntiles + tile] = ll;
+  } else {
+    // scalar-p path: Y, Z, W land unscaled in the CSR rows, then are scaled in place
+    double* ry = cb + (size_t)(q.x >= 0 ? q.x : 0) * K;
+    double* rz = cb + (size_t)(q.y >= 0 ? q.y : 0) * K;
+    double* rw = cb + (size_t)(q.z >= 0 ? q.z : 0) * K;
+    if (q.x >= 0 && !(ablate & 1)) dsum = phase_a<K>(th, p, e, ry, rz, rw);
+    const double d = dsum + eps;
+    const double c = n / d;
+    if (q.x >= 0 && !(ablate & 1)) {
+#pragma unroll
+      for (int g = 0; g < K; ++g) {
+        ry[g] *= c;
+        rz[g] *= c;
+        rw[g] *= c;
+      }
+    }
+    cvec[(size_t)b * n_obs_pad + o] = c;
+    const double ll = block_sum(n * log(d), scratch);
+    if (tid == 0) partL[(size_t)b * ntiles + tile] = ll;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// M1, grid (G + theta_blocks, B), block 256.
+//  blocks [0, G): S accumulation (:1012 npr scatter, factorised):
+//      S_r[a b g] = sum_obs c th_i[a] th_j[b] th_k[g]
+//    workgroup w owns a contiguous, balanced run of 64-observation tiles; each tile's
+//    c*theta_i / theta_j / theta_k rows are staged in LDS and consumed by a register-tiled
+//    outer product (lane = (a, b-chunk) cell block x link group).  Accumulators live in VGPRs
+//    across the whole run and are folded across link groups through LDS in a fixed order once
+//    per rating: G partial rows per rating instead of one per tile.
+//  blocks [G, ...): theta gather (:1016-1018) into theta_new, one wave per gene:
+//      theta_new[g][a] = theta[g][a] * (sum of the gene's contiguous c-scaled rows)[a] / deg[g]
+//    (sum over incidences in ascending CSR order per lane + fixed butterfly: reproducible)
+//    (theta itself is still read by the S blocks of this launch; M2 copies it back).
+// ------------------------------------------------------------------------------------------
+constexpr int M1_NT = 256;
+constexpr int MT_BATCH = 4;  // theta gather: rows in flight per lane
+
+template <int K>
+struct S1Plan {
+  using S = SPlan<K, M1_NT>;
+  static constexpr int K3 = K * K * K;
+  static constexpr int KP = (K + 1) & ~1;
+  static constexpr int RS = (KP % 4 == 2) ? KP : KP + 2;  // conflict-free 16-lane b128 rows
+  static constexpr int STAGE_DBL = 3 * ET * RS;
+  static constexpr int RED_SLOTS = S::LG / 2 < 2 ? S::LG / 2 : 2;
+  static constexpr int RED_DBL = RED_SLOTS * K3;
+  static constexpr int LDS_BYTES = (STAGE_DBL > RED_DBL ? STAGE_DBL : RED_DBL) * 8;
+  static_assert(LDS_BYTES <= LDS_BUDGET, "M1 LDS plan over budget");
+};
+
+template <int K>
+__global__ __launch_bounds__(M1_NT, 3) void m1_kernel(
+    const int4* __restrict__ obs, const int* __restrict__ tile_r, const double* __restrict__ theta,
+    double* __restrict__ theta_new, const double* __restrict__ contrib,
+    const double* __restrict__ cvec, const int* __restrict__ gptr, const int* __restrict__ deg,
+    double* __restrict__ partS, int P, int R, long long n_obs_pad, long long nnz, int G,
+    int ablate) {
+  using SP = typename S1Plan<K>::S;
+  using PL = S1Plan<K>;
+  constexpr int K3 = PL::K3, RS = PL::RS;
+  constexpr int NB = SP::NB, NBC = SP::NBC, NBLK = SP::NBLK, LG = SP::LG;
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+
+  if ((int)blockIdx.x >= G) {  // ---------------------------------------------- theta gather
+    const int g = ((int)blockIdx.x - G) * 4 + (tid >> 6);
+    const int lane = tid & 63;
+    if (g >= P) return;  // wave-uniform
+    // the gene's c-scaled rows are contiguous: rows q0..q1-1, one row (K doubles) per lane
+    const double* __restrict__ cb = contrib + (size_t)b * nnz * K;
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    const int q0 = gptr[g], q1 = gptr[g + 1];
+    for (int qb = q0; qb < q1; qb += 64 * MT_BATCH) {
+      double row[MT_BATCH][K];
+#pragma unroll
+      for (int j = 0; j < MT_BATCH; ++j) {
+        const int qq = qb + j * 64 + lane;
+        const double* __restrict__ src = cb + (size_t)(qq < q1 ? qq : q0) * K;
+#pragma unroll
+        for (int k = 0; k < K; ++k) row[j][k] = qq < q1 ? src[k] : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < MT_BATCH; ++j)
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] += row[j][k];
+    }
+    double mine = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double t = wave_sum(acc[k]);
+      if (lane == k) mine = t;
+    }
+    if (lane < K)
+      theta_new[(size_t)b * P * K + (size_t)g * K + lane] = th[(size_t)g * K + lane] * mine / (double)deg[g];
+    return;
   }
 
-  // ---- phase B: S_r[a b g] = sum_l c_l th_i[a] th_j[b] th_k[g] over this tile
-  double* __restrict__ sdst = partS + ((size_t)b * ntiles + tile) * K3;
-  for (int set = 0; set < ((ablate & 2) ? 0 : SP::NSETS); ++set) {
+  // -------------------------------------------------------------------- S accumulation
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* As = smem;  // c * theta_i rows
+  double* Bs = As + ET * RS;
+  double* Gs = Bs + ET * RS;
+  const int w = blockIdx.x;
+  const int T = (int)(n_obs_pad / ET);
+  const int t0 = (int)((long long)w * T / G), t1 = (int)((long long)(w + 1) * T / G);
+  double* __restrict__ rows = partS + ((size_t)b * G + w) * R * K3;
+  for (int idx = tid; idx < R * K3; idx += M1_NT) rows[idx] = 0.0;  // ratings this run lacks
+  if (ablate & 2) return;
+
+  for (int set = 0; set < SP::NSETS; ++set) {
     int blk, grp;
     if constexpr (SP::NSETS == 1) {
       blk = tid % NBLK;
       grp = tid / NBLK;
     } else {
-      blk = set * NT + tid;
+      blk = set * M1_NT + tid;
       grp = 0;
     }
     const bool active = (grp < LG) && (blk < NBLK);
@@ -492,195 +561,211 @@ __global__ __launch_bounds__((EPlan<K, TS>::NT)) void estep_kernel(
     for (int q = 0; q < NB; ++q)
 #pragma unroll
       for (int g = 0; g < K; ++g) acc[q][g] = 0.0;
-    if (active) {
-#pragma unroll 2
-      for (int l = grp; l < TS; l += LG) {
-        const double av = Cv[l] * Ri[l * RS + alpha];
-        double gv[K];
+
+    // fold the link groups' accumulators (fixed order) and store rating cur_r's row
+    auto flush = [&](int cur_r) {
+      if constexpr (LG > 1) {
+        double* red = smem;  // the staged rows are dead here
+        int ng = LG;
+        while (ng > 1) {
+          const int k = (ng / 2 < PL::RED_SLOTS) ? ng / 2 : PL::RED_SLOTS;
+          __syncthreads();
+          if (active && grp >= ng - k && grp < ng) {
+            double* dst = red + (size_t)(grp - (ng - k)) * K3 + (alpha * K + beta0) * K;
 #pragma unroll
-        for (int g = 0; g < (K & ~1); g += 2) {
-          const double2 v = *reinterpret_cast<const double2*>(Rk + l * RS + g);
-          gv[g] = v.x;
-          gv[g + 1] = v.y;
+            for (int q = 0; q < NB; ++q)
+              if (NB * NBC == K || beta0 + q < K)
+#pragma unroll
+                for (int g = 0; g < K; ++g) dst[q * K + g] = acc[q][g];
+          }
+          __syncthreads();
+          if (active && grp < k) {
+            const double* src = red + (size_t)grp * K3 + (alpha * K + beta0) * K;
+#pragma unroll
+            for (int q = 0; q < NB; ++q)
+              if (NB * NBC == K || beta0 + q < K)
+#pragma unroll
+                for (int g = 0; g < K; ++g) acc[q][g] += src[q * K + g];
+          }
+          ng -= k;
         }
-        if constexpr (K & 1) gv[K - 1] = Rk[l * RS + K - 1];
+      }
+      if (active && grp == 0) {
+        double* dst = rows + (size_t)cur_r * K3 + (alpha * K + beta0) * K;
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-          if (NB * NBC == K || beta0 + q < K) {
-            const double ab = av * Rj[l * RS + beta0 + q];
+        for (int q = 0; q < NB; ++q)
+          if (NB * NBC == K || beta0 + q < K)
 #pragma unroll
-            for (int g = 0; g < K; ++g) acc[q][g] = fma(ab, gv[g], acc[q][g]);
+            for (int g = 0; g < K; ++g) dst[q * K + g] = acc[q][g];
+      }
+#pragma unroll
+      for (int q = 0; q < NB; ++q)
+#pragma unroll
+        for (int g = 0; g < K; ++g) acc[q][g] = 0.0;
+    };
+
+    int cur_r = tile_r[(t0 * ET) / TILE];
+    for (int t = t0; t < t1; ++t) {
+      const int rt = tile_r[(t * ET) / TILE];
+      if (rt != cur_r) {  // workgroup-uniform
+        flush(cur_r);
+        cur_r = rt;
+      }
+      __syncthreads();  // previous tile's readers are done with the stage
+      if (tid < 3 * ET) {
+        const int l = tid % ET, which = tid / ET;
+        const size_t oo = (size_t)t * ET + l;
+        const int4 e = obs[oo];
+        const int gene = which == 0 ? e.x : which == 1 ? e.y : e.z;
+        const double sc = which == 0 ? cvec[(size_t)b * n_obs_pad + oo] : 1.0;
+        const double* __restrict__ src = th + (size_t)gene * K;
+        double* dst = smem + which * ET * RS + l * RS;
+#pragma unroll
+        for (int g = 0; g < K; ++g) dst[g] = sc * src[g];
+      }
+      __syncthreads();
+      if (active) {
+#pragma unroll 1
+        for (int l = grp; l < ET; l += LG) {
+          const double av = As[l * RS + alpha];
+          double gv[K];
+          lds_row<K>(gv, Gs + l * RS);
+#pragma unroll
+          for (int q = 0; q < NB; ++q) {
+            if (NB * NBC == K || beta0 + q < K) {
+              const double ab = av * Bs[l * RS + beta0 + q];
+#pragma unroll
+              for (int g = 0; g < K; ++g) acc[q][g] = fma(ab, gv[g], acc[q][g]);
+            }
           }
         }
       }
     }
-    if constexpr (LG > 1) {
-      double* red = Ri;  // rows are dead once every group has accumulated
-      int ng = LG;
-      while (ng > 1) {
-        const int half = (ng + 1) / 2;
-        __syncthreads();
-        if (active && grp >= half && grp < ng) {
-          double* dst = red + (size_t)(grp - half) * K3 + (alpha * K + beta0) * K;
-#pragma unroll
-          for (int q = 0; q < NB; ++q)
-            if (NB * NBC == K || beta0 + q < K)
-#pragma unroll
-              for (int g = 0; g < K; ++g) dst[q * K + g] = acc[q][g];
-        }
-        __syncthreads();
-        if (active && grp < ng - half) {
-          const double* src = red + (size_t)grp * K3 + (alpha * K + beta0) * K;
-#pragma unroll
-          for (int q = 0; q < NB; ++q)
-            if (NB * NBC == K || beta0 + q < K)
-#pragma unroll
-              for (int g = 0; g < K; ++g) acc[q][g] += src[q * K + g];
-        }
-        ng = half;
-      }
-    }
-    if (active && grp == 0) {
-      double* dst = sdst + (alpha * K + beta0) * K;
-#pragma unroll
-      for (int q = 0; q < NB; ++q)
-        if (NB * NBC == K || beta0 + q < K)
-#pragma unroll
-          for (int g = 0; g < K; ++g) dst[q * K + g] = acc[q][g];
-    }
+    flush(cur_r);
   }
 }
 
-struct Segs {
-  int t[MAX_R + 1];  // tile offsets of each rating group
-};
-
-constexpr int MP_CELLS = 4;   // p M-step: cells per block
-constexpr int MP_PARTS = 64;  // p M-step: tile stripes per cell
-constexpr int MT_BATCH = 4;   // theta M-step: incidences in flight per lane
+// CSR inversion: pos[obs][slot] = the CSR row of (obs, slot); -1 stays on padding rows.
+__global__ void csr_invert_kernel(const int* __restrict__ ginc, long long nnz, int* __restrict__ pos) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nnz) {
+    const int inc = ginc[q];
+    pos[(size_t)(inc / 3) * 4 + inc % 3] = (int)q;
+  }
+}
 
 // ------------------------------------------------------------------------------------------
-// Fused M-step, grid (theta_blocks + ceil(K3 / MP_CELLS), B), block 256.
-//  blocks [0, theta_blocks): theta (:1016-1018), one wave per gene:
-//      theta[g][a] <- theta[g][a] * (sum over the gene's incidences of c * row[a]) / deg[g]
-//    lanes stride the incidence list MT_BATCH entries at a time (all loads of a batch in
-//    flight together), each keeps K partial sums, then a fixed butterfly.
-//  blocks [theta_blocks, ...): p (:1021-1028), MP_CELLS cells x MP_PARTS tile stripes:
-//      S_r = sum of the per-tile partials of rating r; npr_r = p_r S_r;
-//      p_r <- npr_r / (eps + sum_r npr_r).
-// Both halves read only E-step outputs and write disjoint parameters, so they share a launch.
-// Every sum has a fixed order (bitwise reproducible).
+// M2, grid (ceil(K3 / 4) + copy_blocks, B), block 256.
+//  blocks [0, p_blocks): p (:1021-1028), one wave per cell: S_r = sum over the G partial
+//    rows (lane-strided, fixed butterfly); npr_r = p_r S_r; p_r <- npr_r / (eps + sum_r npr_r).
+//  blocks [p_blocks, ...): theta <- theta_new.
 // ------------------------------------------------------------------------------------------
 template <int K>
-__global__ __launch_bounds__(256) void mstep_kernel(
-    double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ contrib,
-    const double* __restrict__ cvec, const int* __restrict__ gptr, const int* __restrict__ ginc,
-    const int* __restrict__ deg, const double* __restrict__ partS, Segs segs, int P, int R,
-    int ntiles, long long n_obs_pad, int theta_blocks, double eps) {
+__global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr,
+                                                 double* __restrict__ theta,
+                                                 const double* __restrict__ theta_new,
+                                                 const double* __restrict__ partS, int P, int R,
+                                                 int G, int p_blocks, double eps) {
   constexpr int K3 = K * K * K;
   const int b = blockIdx.y;
-  if ((int)blockIdx.x < theta_blocks) {
-    const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (g >= P) return;  // wave-uniform
-    const double* __restrict__ cb = contrib + (size_t)b * n_obs_pad * 3 * K;
-    const double* __restrict__ cv = cvec + (size_t)b * n_obs_pad;
-    double acc[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    const int q0 = gptr[g], q1 = gptr[g + 1];
-    for (int qb = q0; qb < q1; qb += 64 * MT_BATCH) {
-      int inc[MT_BATCH];
-#pragma unroll
-      for (int j = 0; j < MT_BATCH; ++j) {
-        const int q = qb + j * 64 + lane;
-        inc[j] = q < q1 ? ginc[q] : -1;
-      }
-      double cc[MT_BATCH], row[MT_BATCH][K];
-#pragma unroll
-      for (int j = 0; j < MT_BATCH; ++j) {
-        const int ij = inc[j] < 0 ? 0 : inc[j];
-        cc[j] = inc[j] < 0 ? 0.0 : cv[ij / 3];
-        const double* __restrict__ src = cb + (size_t)ij * K;
-#pragma unroll
-        for (int k = 0; k < K; ++k) row[j][k] = src[k];
-      }
-#pragma unroll
-      for (int j = 0; j < MT_BATCH; ++j)
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc[k] = fma(cc[j], row[j][k], acc[k]);
-    }
-    double mine = 0.0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double t = wave_sum(acc[k]);
-      if (lane == k) mine = t;
-    }
-    if (lane < K) {
-      double* th = theta + (size_t)b * P * K + (size_t)g * K;
-      th[lane] = th[lane] * mine / (double)deg[g];
-    }
+  if ((int)blockIdx.x >= p_blocks) {
+    const size_t n = (size_t)P * K;
+    const size_t i = ((size_t)blockIdx.x - p_blocks) * 256 + threadIdx.x;
+    if (i < n) theta[(size_t)b * n + i] = theta_new[(size_t)b * n + i];
     return;
   }
-  __shared__ double red[MP_PARTS][MP_CELLS];
-  const int cl = threadIdx.x % MP_CELLS;
-  const int part = threadIdx.x / MP_CELLS;
-  const int cell = ((int)blockIdx.x - theta_blocks) * MP_CELLS + cl;
-  const double* __restrict__ ps = partS + (size_t)b * ntiles * K3 + cell;
-  double S[MAX_R];
+  const int cell = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (cell >= K3) return;  // wave-uniform
+  const double* __restrict__ rows = partS + (size_t)b * G * R * K3 + cell;
+  double npr[MAX_R];
+  double den = eps;
+  double* pc = pr + (size_t)b * R * K3 + cell;
   for (int r = 0; r < R; ++r) {
     double s = 0.0;
-    if (cell < K3) {
-      const int end = segs.t[r + 1];
-      int t = segs.t[r] + part;
-      for (; t + 3 * MP_PARTS < end; t += 4 * MP_PARTS) {
-        const double a0 = ps[(size_t)t * K3], a1 = ps[(size_t)(t + MP_PARTS) * K3];
-        const double a2 = ps[(size_t)(t + 2 * MP_PARTS) * K3], a3 = ps[(size_t)(t + 3 * MP_PARTS) * K3];
-        s += (a0 + a1) + (a2 + a3);
-      }
-      for (; t < end; t += MP_PARTS) s += ps[(size_t)t * K3];
-    }
-    red[part][cl] = s;
-    __syncthreads();
-    double tot = 0.0;
-    if (part == 0)
-      for (int q = 0; q < MP_PARTS; ++q) tot += red[q][cl];
-    S[r] = tot;
-    __syncthreads();
+    for (int w = lane; w < G; w += 64) s += rows[((size_t)w * R + r) * K3];
+    s = wave_sum(s);
+    npr[r] = pc[(size_t)r * K3] * s;
+    den += npr[r];
   }
-  if (part == 0 && cell < K3) {
-    double* pc = pr + (size_t)b * R * K3;
-    double npr[MAX_R];
-    double den = eps;
-    for (int r = 0; r < R; ++r) {
-      npr[r] = pc[(size_t)r * K3 + cell] * S[r];
-      den += npr[r];
-    }
-    for (int r = 0; r < R; ++r) pc[(size_t)r * K3 + cell] = npr[r] / den;
-  }
+  if (lane == 0)
+    for (int r = 0; r < R; ++r) pc[(size_t)r * K3] = npr[r] / den;
 }
 
 // ------------------------------------------------------------------------------------------
-// Log-likelihood tile partials (:958-969): grid (ntiles, B), block TILE.
+// Log-likelihood partials (:958-969), one per 64-observation tile: grid (n_obs_pad/64, B).
+//  K in the LDS plan: 128 threads, p_r staged in LDS, two lanes per observation (a halves);
+//  otherwise 64 threads, p_r through the scalar cache.
 // ------------------------------------------------------------------------------------------
+constexpr int LL_TS = ET;
+
 template <int K>
-__global__ __launch_bounds__(TILE) void loglik_kernel(const int4* __restrict__ obs,
-                                                      const int* __restrict__ tile_r,
-                                                      const double* __restrict__ theta,
-                                                      const double* __restrict__ pr,
-                                                      double* __restrict__ partL, int P, int R,
-                                                      int ntiles, double eps) {
-  __shared__ double scratch[TILE / 64];
-  constexpr int K3 = K * K * K;
+__global__ __launch_bounds__((EPlan<K>::NT)) void loglik_kernel(
+    const int4* __restrict__ obs, const int* __restrict__ tile_r, const double* __restrict__ theta,
+    const double* __restrict__ pr, double* __restrict__ partL, int P, int R, int ntiles,
+    double eps) {
+  using EP = EPlan<K>;
+  constexpr int K3 = K * K * K, KP = EP::KP, KH = EP::KH, H = EP::H, NT = EP::NT;
+  __shared__ __attribute__((aligned(16))) double Ps[EP::STAGE_P ? EP::P_DBL : 2];
+  __shared__ double scratch[8];
   const int tile = blockIdx.x;
   const int b = blockIdx.y;
-  const int r = __builtin_amdgcn_readfirstlane(tile_r[tile]);
+  const int tid = threadIdx.x;
+  const int lo = tid / H, h = tid % H;
+  const int r = __builtin_amdgcn_readfirstlane(tile_r[(tile * LL_TS) / TILE]);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-  const int4 e = obs[(size_t)tile * TILE + threadIdx.x];
-  const double d = contract<K>(th, p, e.x, e.y, e.z) + eps;
-  const double ll = block_sum((double)e.w * log(d), scratch);
-  if (threadIdx.x == 0) partL[(size_t)b * ntiles + tile] = ll;
+  const int4 e = obs[(size_t)tile * LL_TS + lo];
+  double dsum;
+  if constexpr (EP::STAGE_P) {
+    stage_p<K>(Ps, p, tid, NT);
+    __syncthreads();
+    const double* __restrict__ ri = th + (size_t)e.x * K;
+    const double* __restrict__ rj = th + (size_t)e.y * K;
+    const double* __restrict__ rk = th + (size_t)e.z * K;
+    double tj[K], tk[K];
+#pragma unroll
+    for (int g = 0; g < K; ++g) {
+      tj[g] = rj[g];
+      tk[g] = rk[g];
+    }
+    dsum = 0.0;
+#pragma unroll 1
+    for (int q = 0; q < KH; ++q) {
+      const int a = h * KH + q;
+      const bool valid = a < K;
+      const int ac = valid ? a : K - 1;
+      const double ta = valid ? ri[ac] : 0.0;
+      const double* __restrict__ pa = Ps + EP::slab(ac);
+      double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+      for (int bb = 0; bb < K; bb += 2) {
+        double u0 = 0.0, u1 = 0.0;
+#pragma unroll
+        for (int g = 0; g < (K & ~1); g += 2) {
+          const double2 v0 = *reinterpret_cast<const double2*>(pa + bb * KP + g);
+          u0 = fma(v0.y, tk[g + 1], fma(v0.x, tk[g], u0));
+          if (bb + 1 < K) {
+            const double2 v1 = *reinterpret_cast<const double2*>(pa + (bb + 1) * KP + g);
+            u1 = fma(v1.y, tk[g + 1], fma(v1.x, tk[g], u1));
+          }
+        }
+        if constexpr (K & 1) {
+          u0 = fma(pa[bb * KP + K - 1], tk[K - 1], u0);
+          if (bb + 1 < K) u1 = fma(pa[(bb + 1) * KP + K - 1], tk[K - 1], u1);
+        }
+        y0 = fma(tj[bb], u0, y0);
+        if (bb + 1 < K) y1 = fma(tj[bb + 1], u1, y1);
+      }
+      dsum = fma(ta, y0 + y1, dsum);
+    }
+    dsum += __shfl_xor(dsum, 1, 64);  // partner lane's a-half (commutative: lanes agree)
+  } else {
+    dsum = contract<K>(th, p, e.x, e.y, e.z);
+  }
+  const double d = dsum + eps;
+  const double ll = block_sum(h == 0 ? (double)e.w * log(d) : 0.0, scratch);
+  if (tid == 0) partL[(size_t)b * ntiles + tile] = ll;
 }
 
 // Fixed-order sum of per-tile partials: grid (B), block 256.
@@ -725,8 +810,9 @@ struct LinkSet {
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Launch {
-  int (*estep)(mmsbm_ctx*, const double*, const double*, hipStream_t);
-  int (*mstep)(mmsbm_ctx*, hipStream_t);
+  int (*estep)(mmsbm_ctx*, hipStream_t);
+  int (*m1)(mmsbm_ctx*, hipStream_t);
+  int (*m2)(mmsbm_ctx*, hipStream_t);
   int (*loglik)(mmsbm_ctx*, int, const double*, const double*, hipStream_t);
   int (*predict)(mmsbm_ctx*, const int*, long long, const double*, const double*, double*,
                  hipStream_t);
@@ -741,6 +827,7 @@ struct mmsbm_ctx {
   LinkSet sets[2];
   const int* gptr = nullptr;
   const int* ginc = nullptr;
+  int* pos = nullptr;  // device, owned: [n_obs_pad][4] CSR rows of each observation's slots
   const int* deg = nullptr;
   long long nnz = 0;
   bool genes_set = false;
@@ -751,22 +838,32 @@ struct mmsbm_ctx {
   double* cvec = nullptr;
   double* partS = nullptr;
   double* partL = nullptr;
+  double* theta_new = nullptr;
   // current iterate (only valid during a call)
   double* theta_mut = nullptr;
   double* pr_mut = nullptr;
   // optional per-kernel timing: HIP event pairs recorded around each launch on its stream
   bool timing = false;
+  int timing_stride = 1;  // time every n-th iteration
   int ablate = 0;  // MMSBM_ABLATE (measurement only)
-  int ts = 64;     // E-step tile (observations per workgroup): MMSBM_ESTEP_TILE = 64/128/256
-  std::vector<hipEvent_t> ev[2];  // start/stop pairs per kernel id
-  size_t nev[2] = {0, 0};
+  int sacc_wgs = SACC_WGS;  // S-accumulation workgroups requested (MMSBM_SACC_WGS)
+  std::vector<hipEvent_t> ev[3];  // start/stop pairs per kernel id (E, M1, M2)
+  size_t nev[3] = {0, 0, 0};
 };
 
 namespace {
 
 struct WsLayout {
-  size_t contrib, cvec, partS, partL, total;
+  size_t contrib, cvec, partS, partL, theta_new, total;
 };
+
+// S-accumulation workgroups actually launched: never more than the train set's tiles.
+int sacc_groups(const mmsbm_ctx* c) {
+  const long long T = c->sets[MMSBM_SET_TRAIN].n_obs_pad / ET;
+  long long G = c->sacc_wgs < SACC_WGS_MAX ? c->sacc_wgs : SACC_WGS_MAX;
+  if (G > T) G = T;
+  return (int)(G > 0 ? G : 1);
+}
 
 WsLayout ws_layout(const mmsbm_ctx* c) {
   WsLayout L{};
@@ -774,70 +871,57 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   const LinkSet& te = c->sets[MMSBM_SET_TEST];
   const size_t K3 = (size_t)c->K * c->K * c->K;
   size_t off = 0;
-  L.contrib = off;
+  L.contrib = off;  // c-scaled (Y, Z, W) rows in gene-CSR order, 3 per observation
   off += align_up((size_t)c->B * tr.n_obs_pad * 3 * c->K * sizeof(double));
   L.cvec = off;
   off += align_up((size_t)c->B * tr.n_obs_pad * sizeof(double));
-  L.partS = off;  // one row per E-step tile; sized for the smallest tile (MIN_TS)
-  const long long et = tr.n_obs_pad / MIN_TS;
-  off += align_up((size_t)c->B * et * K3 * sizeof(double));
-  L.partL = off;
-  long long nt = et > te.ntiles ? et : te.ntiles;
+  L.partS = off;  // [B][G][R][K3] partial S rows of the M1 workgroups
+  off += align_up((size_t)c->B * sacc_groups(c) * c->R * K3 * sizeof(double));
+  L.partL = off;  // one log-likelihood partial per 64-observation tile of either set
+  long long nt = (tr.n_obs_pad > te.n_obs_pad ? tr.n_obs_pad : te.n_obs_pad) / ET;
   off += align_up((size_t)c->B * (nt > 0 ? nt : 1) * sizeof(double));
+  L.theta_new = off;
+  off += align_up((size_t)c->B * c->P * c->K * sizeof(double));
   L.total = off;
   return L;
 }
 
-// E-step tile actually used for a requested one: the largest that fits the LDS plan.
 template <int K>
-int estep_tile(int requested) {
-  if (requested >= 256 && EPlan<K, 256>::FITS) return 256;
-  if (requested >= 128 && EPlan<K, 128>::FITS) return 128;
-  return 64;
-}
-
-template <int K, int TS>
-int launch_estep_ts(mmsbm_ctx* c, hipStream_t s) {
-  using T = EPlan<K, TS>;
-  static_assert(T::FITS, "E-step LDS plan over budget");
+int launch_estep(mmsbm_ctx* c, hipStream_t s) {
+  using EP = EPlan<K>;
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
-  const int et = (int)(tr.n_obs_pad / TS);
-  estep_kernel<K, TS><<<dim3(et, c->B), T::NT, T::LDS_BYTES, s>>>(
-      tr.obs, tr.tile_r, c->theta_mut, c->pr_mut, c->contrib, c->cvec, c->partS, c->partL, c->P,
-      c->R, tr.n_obs_pad, et, c->eps, c->ablate);
+  if (tr.ntiles == 0) return MMSBM_OK;
+  const int nt = (int)(tr.n_obs_pad / ET);
+  estep_kernel<K><<<dim3(nt, c->B), EP::NT, EP::LDS_BYTES, s>>>(
+      tr.obs, reinterpret_cast<const int4*>(c->pos), tr.tile_r, c->theta_mut, c->pr_mut,
+      c->contrib, c->cvec, c->partL, c->P, c->R, tr.n_obs_pad, c->nnz, nt, c->eps, c->ablate);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
 
 template <int K>
-int launch_estep(mmsbm_ctx* c, const double*, const double*, hipStream_t s) {
+int launch_m1(mmsbm_ctx* c, hipStream_t s) {
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
   if (tr.ntiles == 0) return MMSBM_OK;
-  switch (estep_tile<K>(c->ts)) {
-    case 256:
-      if constexpr (EPlan<K, 256>::FITS) return launch_estep_ts<K, 256>(c, s);
-      break;
-    case 128:
-      if constexpr (EPlan<K, 128>::FITS) return launch_estep_ts<K, 128>(c, s);
-      break;
-    default:
-      break;
-  }
-  return launch_estep_ts<K, 64>(c, s);
+  const int G = sacc_groups(c);
+  const int theta_blocks = (c->P + 3) / 4;
+  m1_kernel<K><<<dim3(G + theta_blocks, c->B), M1_NT, S1Plan<K>::LDS_BYTES, s>>>(
+      tr.obs, tr.tile_r, c->theta_mut, c->theta_new, c->contrib, c->cvec, c->gptr, c->deg,
+      c->partS, c->P, c->R, tr.n_obs_pad, c->nnz, G, c->ablate);
+  HIP_TRY(hipGetLastError());
+  return MMSBM_OK;
 }
 
 template <int K>
-int launch_mstep(mmsbm_ctx* c, hipStream_t s) {
+int launch_m2(mmsbm_ctx* c, hipStream_t s) {
   constexpr int K3 = K * K * K;
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
-  const int ts = estep_tile<K>(c->ts);
-  Segs segs{};  // rating groups in units of E-step tiles
-  for (int r = 0; r <= c->R; ++r) segs.t[r] = (int)(tr.seg.empty() ? 0 : tr.seg[r] / ts);
-  const int theta_blocks = (c->P + 3) / 4;
-  const int p_blocks = (K3 + MP_CELLS - 1) / MP_CELLS;
-  mstep_kernel<K><<<dim3(theta_blocks + p_blocks, c->B), 256, 0, s>>>(
-      c->theta_mut, c->pr_mut, c->contrib, c->cvec, c->gptr, c->ginc, c->deg, c->partS, segs,
-      c->P, c->R, (int)(tr.n_obs_pad / ts), tr.n_obs_pad, theta_blocks, c->eps);
+  if (tr.ntiles == 0) return MMSBM_OK;
+  const int p_blocks = (K3 + 3) / 4;
+  const int copy_blocks = (int)(((long long)c->P * K + 255) / 256);
+  m2_kernel<K><<<dim3(p_blocks + copy_blocks, c->B), 256, 0, s>>>(
+      c->pr_mut, c->theta_mut, c->theta_new, c->partS, c->P, c->R, sacc_groups(c), p_blocks,
+      c->eps);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -846,8 +930,9 @@ template <int K>
 int launch_loglik(mmsbm_ctx* c, int which, const double* theta, const double* pr, hipStream_t s) {
   const LinkSet& ls = c->sets[which];
   if (ls.ntiles == 0) return MMSBM_OK;
-  loglik_kernel<K><<<dim3(ls.ntiles, c->B), TILE, 0, s>>>(ls.obs, ls.tile_r, theta, pr, c->partL,
-                                                         c->P, c->R, ls.ntiles, c->eps);
+  const int nt = (int)(ls.n_obs_pad / LL_TS);
+  loglik_kernel<K><<<dim3(nt, c->B), EPlan<K>::NT, 0, s>>>(
+      ls.obs, ls.tile_r, theta, pr, c->partL, c->P, c->R, nt, c->eps);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -865,7 +950,8 @@ int launch_predict(mmsbm_ctx* c, const int* ids, long long n, const double* thet
 template <int... Ks>
 constexpr auto make_table(std::integer_sequence<int, Ks...>) {
   return std::array<Launch, sizeof...(Ks)>{
-      Launch{&launch_estep<Ks + 1>, &launch_mstep<Ks + 1>, &launch_loglik<Ks + 1>, &launch_predict<Ks + 1>}...};
+      Launch{&launch_estep<Ks + 1>, &launch_m1<Ks + 1>, &launch_m2<Ks + 1>, &launch_loglik<Ks + 1>,
+             &launch_predict<Ks + 1>}...};
 }
 
 const auto kTable = make_table(std::make_integer_sequence<int, MMSBM_MAX_K>{});
@@ -907,9 +993,9 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   auto* c = new mmsbm_ctx();
   c->device = device;
   if (const char* ab = getenv("MMSBM_ABLATE")) c->ablate = atoi(ab);
-  if (const char* t = getenv("MMSBM_ESTEP_TILE")) {
+  if (const char* t = getenv("MMSBM_SACC_WGS")) {
     const int v = atoi(t);
-    if (v == 64 || v == 128 || v == 256) c->ts = v;
+    if (v >= 1) c->sacc_wgs = v;
   }
   *out = c;
   return MMSBM_OK;
@@ -920,6 +1006,7 @@ int mmsbm_destroy(mmsbm_ctx* c) {
   (void)hipSetDevice(c->device);
   for (auto& s : c->sets)
     if (s.tile_r) (void)hipFree(s.tile_r);
+  if (c->pos) (void)hipFree(c->pos);
   for (auto& v : c->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   delete c;
@@ -978,6 +1065,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* obs, int64_t n_o
     HIP_TRY(hipMemcpy(ls.tile_r, tr.data(), tr.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   ls.obs = reinterpret_cast<const int4*>(obs);
+  if (which == MMSBM_SET_TRAIN) c->genes_set = false;  // the incidence CSR must follow
   ls.n_obs_pad = n_obs_pad;
   ls.ntiles = (int)(n_obs_pad / TILE);
   ls.seg = seg;
@@ -995,6 +1083,23 @@ int mmsbm_set_genes(mmsbm_ctx* c, const int32_t* gene_ptr, const int32_t* gene_i
   c->zero_degree = false;
   for (int g = 0; g < c->P; ++g)
     if (hdeg[g] <= 0) c->zero_degree = true;
+  const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
+  if (nnz > 3 * tr.n_obs_pad)
+    return fail(MMSBM_ERR_INVALID, "nnz=%lld exceeds 3 x train rows: call mmsbm_set_links(TRAIN) first",
+                (long long)nnz);
+  if (c->pos) {
+    HIP_TRY(hipFree(c->pos));
+    c->pos = nullptr;
+  }
+  if (tr.n_obs_pad > 0) {
+    HIP_TRY(hipMalloc(&c->pos, sizeof(int) * 4 * tr.n_obs_pad));
+    HIP_TRY(hipMemset(c->pos, 0xFF, sizeof(int) * 4 * tr.n_obs_pad));
+    if (nnz > 0) {
+      csr_invert_kernel<<<(unsigned)((nnz + 255) / 256), 256>>>(gene_inc, nnz, c->pos);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipDeviceSynchronize());
+  }
   c->gptr = gene_ptr;
   c->ginc = gene_inc;
   c->deg = deg;
@@ -1024,6 +1129,7 @@ int mmsbm_set_workspace(mmsbm_ctx* c, void* ws, int64_t bytes) {
   c->cvec = (double*)(c->ws + L.cvec);
   c->partS = (double*)(c->ws + L.partS);
   c->partL = (double*)(c->ws + L.partL);
+  c->theta_new = (double*)(c->ws + L.theta_new);
   return MMSBM_OK;
 }
 
@@ -1044,12 +1150,16 @@ int mmsbm_iterate(mmsbm_ctx* c, double* theta, double* pr, int32_t n_iters, void
   c->theta_mut = theta;
   c->pr_mut = pr;
   for (int it = 0; it < n_iters; ++it) {
-    if ((rc = timing_mark(c, 0, s))) return rc;
-    if ((rc = L.estep(c, theta, pr, s))) return rc;
-    if ((rc = timing_mark(c, 0, s))) return rc;
-    if ((rc = timing_mark(c, 1, s))) return rc;
-    if ((rc = L.mstep(c, s))) return rc;
-    if ((rc = timing_mark(c, 1, s))) return rc;
+    const bool mark = c->timing && (it % c->timing_stride == 0);
+    if (mark && (rc = timing_mark(c, 0, s))) return rc;
+    if ((rc = L.estep(c, s))) return rc;
+    if (mark && (rc = timing_mark(c, 0, s))) return rc;
+    if (mark && (rc = timing_mark(c, 1, s))) return rc;
+    if ((rc = L.m1(c, s))) return rc;
+    if (mark && (rc = timing_mark(c, 1, s))) return rc;
+    if (mark && (rc = timing_mark(c, 2, s))) return rc;
+    if ((rc = L.m2(c, s))) return rc;
+    if (mark && (rc = timing_mark(c, 2, s))) return rc;
   }
   return MMSBM_OK;
 }
@@ -1071,7 +1181,7 @@ int mmsbm_loglik(mmsbm_ctx* c, int32_t which, const double* theta, const double*
     return MMSBM_OK;
   }
   if ((rc = kTable[c->K - 1].loglik(c, which, theta, pr, s))) return rc;
-  reduce_kernel<<<c->B, 256, 0, s>>>(c->partL, ls.ntiles, out);
+  reduce_kernel<<<c->B, 256, 0, s>>>(c->partL, (int)(ls.n_obs_pad / LL_TS), out);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -1087,16 +1197,17 @@ int mmsbm_predict(mmsbm_ctx* c, const int32_t* ids, int64_t n, const double* the
   return kTable[c->K - 1].predict(c, ids, n, theta, pr, out, (hipStream_t)stream);
 }
 
-int mmsbm_timing(mmsbm_ctx* c, int32_t enable) {
+int mmsbm_timing(mmsbm_ctx* c, int32_t stride) {
   if (!c) return fail(MMSBM_ERR_INVALID, "null context");
-  c->timing = enable != 0;
+  c->timing = stride > 0;
+  c->timing_stride = stride > 0 ? stride : 1;
   for (auto& n : c->nev) n = 0;
   return MMSBM_OK;
 }
 
 int mmsbm_timing_result(mmsbm_ctx* c, int32_t kernel, double* total_ms, int64_t* count) {
   if (!c || !total_ms || !count) return fail(MMSBM_ERR_INVALID, "null argument");
-  if (kernel < 0 || kernel > 1) return fail(MMSBM_ERR_INVALID, "kernel id %d", kernel);
+  if (kernel < 0 || kernel > 2) return fail(MMSBM_ERR_INVALID, "kernel id %d", kernel);
   const size_t n = c->nev[kernel] / 2;
   double tot = 0.0;
   if (n) HIP_TRY(hipEventSynchronize(c->ev[kernel][2 * n - 1]));

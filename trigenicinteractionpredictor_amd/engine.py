@@ -122,11 +122,11 @@ class EMEngine:
         return out[:, :n].cpu().numpy()
 
     # ---------------------------------------------------------- measurement
-    KERNELS = ("estep", "mstep")
+    KERNELS = ("estep", "m1", "m2")
 
-    def timing(self, enable: bool = True):
-        """Record HIP event pairs around every kernel launched by iterate()."""
-        _lib.check(self.lib.mmsbm_timing(self.ctx, 1 if enable else 0))
+    def timing(self, stride: int = 1):
+        """Record HIP event pairs around the kernels of every `stride`-th iteration (0: off)."""
+        _lib.check(self.lib.mmsbm_timing(self.ctx, int(stride)))
 
     def timing_result(self, kernel: str = "estep"):
         """-> (summed device ms, launches) of one kernel since timing(True)."""
