@@ -116,6 +116,39 @@ def test_against_c_oracle(tmp_path, K, P, E, iters):
     np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
 
 
+@pytest.mark.parametrize("K", [3, 10, 13])
+@pytest.mark.parametrize("groups", ["1", "5", "2048"])
+def test_s_accumulation_workgroup_splits(tmp_path, monkeypatch, K, groups):
+    """M1 with one workgroup (many windows, every rating boundary inside it), a few, and one
+    tile per workgroup: all equal the oracle."""
+    monkeypatch.setenv("MMSBM_SACC_WGS", groups)
+    tr, te = _fold(tmp_path, 300, 12000, seed=K, multi_frac=0.05, both_frac=0.02)
+    m = _gpu_model(tr, te)
+    random.seed(K + 1)
+    m.initialize_parameters(K)
+    theta0, pr0 = np.array(m.theta), np.array(m.pr)
+    m.make_iterations(2)
+    th_o, pr_o, L_o, _ = _oracle_run(m, theta0, pr0, 2)
+    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
+
+
+def test_estep_variants_agree(tmp_path, monkeypatch):
+    """The two E-step kernels (4-lane default, MMSBM_ESTEP=1) both match the oracle."""
+    tr, te = _fold(tmp_path, 400, 8000, seed=21, multi_frac=0.05)
+    for variant in ("0", "1"):
+        monkeypatch.setenv("MMSBM_ESTEP", variant)
+        m = _gpu_model(tr, te)
+        random.seed(3)
+        m.initialize_parameters(8)
+        theta0, pr0 = np.array(m.theta), np.array(m.pr)
+        m.make_iterations(2)
+        th_o, pr_o, _, _ = _oracle_run(m, theta0, pr0, 2)
+        np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+
+
 def test_batched_samples_match_single_runs(tmp_path):
     from trigenicinteractionpredictor_amd import EMEngine, Model
     from trigenicinteractionpredictor_amd.layout import links_to_arrays

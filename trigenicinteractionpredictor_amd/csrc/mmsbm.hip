@@ -1,7 +1,7 @@
 // mmsbm.hip — MI355X (gfx950) MMSBM EM engine: kernels + C ABI (include/mmsbm.h).
 //
 // Hot path of AleixMT/TrigenicInteractionPredictor, src/TrigenicInteractionPredictor.py:
-//   make_iteration      :984-1043   -> estep_kernel, m1_kernel (S, theta gather), m2_kernel (p)
+//   make_iteration      :984-1043   -> estep*_kernel, m1_kernel (S), m2_kernel (p, theta)
 //   compute_likelihood  :952-974    -> loglik_kernel + reduce_kernel
 //   do_prediction       :530-547    -> predict_kernel
 //
@@ -50,7 +50,7 @@ namespace {
 constexpr int TILE = MMSBM_TILE;
 constexpr int MAX_R = 8;
 constexpr int LDS_BUDGET = 64 * 1024;
-constexpr int SACC_WGS = 256;      // default S-accumulation workgroups (MMSBM_SACC_WGS)
+constexpr int SACC_WGS = 256;      // default S-accumulation workgroups (MMSBM_SACC_WGS): 1 per CU
 constexpr int SACC_WGS_MAX = 2048;
 
 thread_local std::string g_err;
@@ -87,10 +87,22 @@ constexpr int pick_nb(int K) {
 }
 
 // Phase-B (S accumulation) tiling for NT threads: lane = (cell block, link group).
-template <int K, int NT>
+// b-chunk per lane for a cell budget of `cells` doubles: a divisor of K when one comes close
+// to the budget (no ragged chunk), else the largest chunk that fits.
+constexpr int pick_nb_cap(int K, int cells) {
+  int cap = cells / K;
+  if (cap < 1) cap = 1;
+  if (cap > K) cap = K;
+  int best = 1;
+  for (int d = 1; d <= cap; ++d)
+    if (K % d == 0) best = d;
+  return (4 * best >= 3 * cap) ? best : cap;
+}
+
+template <int K, int NT, int CELLS = 50>
 struct SPlan {
   static constexpr int K3 = K * K * K;
-  static constexpr int NB = pick_nb(K);    // b-chunk per lane
+  static constexpr int NB = pick_nb_cap(K, CELLS);  // b-chunk per lane
   static constexpr int NBC = (K + NB - 1) / NB;
   static constexpr int NBLK = K * NBC;     // cell blocks (a, b-chunk, all g)
   static constexpr int NSETS = (NBLK + NT - 1) / NT;
@@ -274,6 +286,11 @@ struct EPlan {
   static constexpr int LDS_BYTES = (P_DBL + 8) * 8;
   // waves/SIMD the register allocator must leave room for (3 keeps a fold0 grid resident)
   static constexpr int OCC = STAGE_P ? 3 : 1;
+  // observations per lane in the E-step (two halve the LDS reads per FMA and double the
+  // independent FMA chains; the fold0 grid is then one wave per SIMD, latency covered by ILP)
+  static constexpr int NO = STAGE_P && K >= 4 && K <= 10 ? 2 : 1;
+  static constexpr int EOBS = ET * NO;  // observations per E-step workgroup
+  static constexpr int E_OCC = NO == 2 ? 2 : OCC;
   __device__ static constexpr int slab(int a) { return a * K * KP + (a >= KH ? 2 : 0); }
 };
 
@@ -298,37 +315,42 @@ __device__ __forceinline__ void lds_row(double (&dst)[K], const double* __restri
   if constexpr (K & 1) dst[K - 1] = src[K - 1];
 }
 
-// Phase A with p_r in LDS, lane h of 2 covering a in [h*KH, h*KH + KH).  Returns Y[a] of its
-// own a-range in yv; on return zc / wc / dsum hold the FULL sums (partner partials added
-// in a commutative, lane-symmetric order, so both lanes agree bitwise).
-template <int K>
-__device__ __forceinline__ double phase_a_lds(const double* __restrict__ Ps,
-                                              const double* __restrict__ ri,
-                                              const double* __restrict__ rj,
-                                              const double* __restrict__ rk, int h,
-                                              double (&yv)[EPlan<K>::KH], double (&zc)[K],
-                                              double (&wc)[K]) {
+// Phase A with p_r in LDS for NO observations per lane; lane h of 2 covers a in
+// [h*KH, h*KH + KH).  Returns Y[a] of its own a-range in yv; on return zc / wc / dsum hold the
+// FULL sums (partner partials added in a commutative, lane-symmetric order, so both lanes
+// agree bitwise).  Every p value read from LDS feeds 2*NO FMAs.
+template <int K, int NO>
+__device__ __forceinline__ void phase_a_lds(const double* __restrict__ Ps,
+                                            const double* __restrict__ const (&ri)[NO],
+                                            const double* __restrict__ const (&rj)[NO],
+                                            const double* __restrict__ const (&rk)[NO], int h,
+                                            double (&yv)[NO][EPlan<K>::KH], double (&zc)[NO][K],
+                                            double (&wc)[NO][K], double (&dsum)[NO]) {
   using EP = EPlan<K>;
   constexpr int KP = EP::KP, KH = EP::KH, NPAIR = (K + 1) / 2;
-  double tj[K], tk[K], ti[KH];
+  double tj[NO][K], tk[NO][K], ti[NO][KH];
 #pragma unroll
-  for (int g = 0; g < K; ++g) {
-    tj[g] = rj[g];
-    tk[g] = rk[g];
-    zc[g] = 0.0;
-    wc[g] = 0.0;
+  for (int m = 0; m < NO; ++m) {
+#pragma unroll
+    for (int g = 0; g < K; ++g) {
+      tj[m][g] = rj[m][g];
+      tk[m][g] = rk[m][g];
+      zc[m][g] = 0.0;
+      wc[m][g] = 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < KH; ++q) ti[m][q] = (h * KH + q < K) ? ri[m][h * KH + q] : 0.0;
+    dsum[m] = 0.0;
   }
-#pragma unroll
-  for (int q = 0; q < KH; ++q) ti[q] = (h * KH + q < K) ? ri[h * KH + q] : 0.0;
-  double dsum = 0.0;
-  // Two p rows per step: two independent U chains for ILP.
+  // Two p rows per step: 2*NO independent U chains.
 #pragma unroll
   for (int q = 0; q < KH; ++q) {
     const int a = h * KH + q;
     const bool valid = a < K;
-    const double ta = ti[q];
     const double* __restrict__ pa = Ps + EP::slab(valid ? a : K - 1);
-    double y = 0.0;
+    double y[NO];
+#pragma unroll
+    for (int m = 0; m < NO; ++m) y[m] = 0.0;
 #pragma unroll
     for (int bp = 0; bp < NPAIR; ++bp) {
       const int b0 = 2 * bp, b1 = 2 * bp + 1;
@@ -340,36 +362,215 @@ __device__ __forceinline__ double phase_a_lds(const double* __restrict__ Ps,
 #pragma unroll
         for (int g = 0; g < K; ++g) pv1[g] = 0.0;
       }
-      double u0 = 0.0, u1 = 0.0;
 #pragma unroll
-      for (int g = 0; g < K; ++g) {
-        u0 = fma(pv0[g], tk[g], u0);
-        u1 = fma(pv1[g], tk[g], u1);
-      }
-      const double t0 = ta * tj[b0];
-      y = fma(tj[b0], u0, y);
-      zc[b0] = fma(ta, u0, zc[b0]);
-      if (b1 < K) {
-        const double t1 = ta * tj[b1];
-        y = fma(tj[b1], u1, y);
-        zc[b1] = fma(ta, u1, zc[b1]);
+      for (int m = 0; m < NO; ++m) {
+        const double ta = ti[m][q];
+        double u0 = 0.0, u1 = 0.0;
 #pragma unroll
-        for (int g = 0; g < K; ++g) wc[g] = fma(t1, pv1[g], fma(t0, pv0[g], wc[g]));
-      } else {
+        for (int g = 0; g < K; ++g) {
+          u0 = fma(pv0[g], tk[m][g], u0);
+          u1 = fma(pv1[g], tk[m][g], u1);
+        }
+        const double t0 = ta * tj[m][b0];
+        y[m] = fma(tj[m][b0], u0, y[m]);
+        zc[m][b0] = fma(ta, u0, zc[m][b0]);
+        if (b1 < K) {
+          const double t1 = ta * tj[m][b1];
+          y[m] = fma(tj[m][b1], u1, y[m]);
+          zc[m][b1] = fma(ta, u1, zc[m][b1]);
 #pragma unroll
-        for (int g = 0; g < K; ++g) wc[g] = fma(t0, pv0[g], wc[g]);
+          for (int g = 0; g < K; ++g) wc[m][g] = fma(t1, pv1[g], fma(t0, pv0[g], wc[m][g]));
+        } else {
+#pragma unroll
+          for (int g = 0; g < K; ++g) wc[m][g] = fma(t0, pv0[g], wc[m][g]);
+        }
       }
     }
-    yv[q] = y;
+#pragma unroll
+    for (int m = 0; m < NO; ++m) {
+      yv[m][q] = y[m];
+      dsum[m] = fma(ti[m][q], y[m], dsum[m]);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < NO; ++m) {
+#pragma unroll
+    for (int g = 0; g < K; ++g) {
+      zc[m][g] += __shfl_xor(zc[m][g], 1, 64);
+      wc[m][g] += __shfl_xor(wc[m][g], 1, 64);
+    }
+    dsum[m] += __shfl_xor(dsum[m], 1, 64);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// E-step, four lanes per observation: lane h = (ha, hb) covers the a-half ha x b-half hb block
+// of the (a, b) lattice (balanced for every even K), so a fold0-sized problem has ~4 waves per
+// SIMD; FP64 FMA needs >= 4 resident waves with >= 4 independent chains each to approach its
+// issue rate (one wave alone issues at most one per ~6.5 cycles; dependent latency ~40).
+// p_r in LDS: the four lanes of an observation read four different (a, b) rows per
+// instruction; the half offsets sa / sb place them in four distinct 4-bank slots.
+// ------------------------------------------------------------------------------------------
+constexpr int E4_NT = 256;  // 64 observations x 4 lanes
+
+constexpr bool e4_slots_ok(int K, int sa, int sb) {
+  const int KP = (K + 1) & ~1, KA = (K + 1) / 2, KB = (K + 1) / 2, SA = K * KP + 8;
+  const int da = ((KA * SA + sa) / 2) % 16, db = ((KB * KP + sb) / 2) % 16;
+  return da != 0 && db != 0 && da != db && (da + db) % 16 != 0;
+}
+constexpr int e4_pick_sa(int K) {
+  for (int sa = 0; sa <= 30; sa += 2)
+    for (int sb = 0; sb <= 6; sb += 2)
+      if (e4_slots_ok(K, sa, sb)) return sa;
+  return 0;
+}
+constexpr int e4_pick_sb(int K) {
+  for (int sa = 0; sa <= 30; sa += 2)
+    for (int sb = 0; sb <= 6; sb += 2)
+      if (e4_slots_ok(K, sa, sb)) return sb;
+  return 0;
+}
+
+template <int K>
+struct E4Plan {
+  static constexpr bool ON = K >= 2 && K <= 12 && K != 9 && K != 11;
+  static constexpr int K3 = K * K * K;
+  static constexpr int KP = (K + 1) & ~1;
+  static constexpr int KA = (K + 1) / 2, KB = (K + 1) / 2;
+  static constexpr int SA = K * KP + 8;  // a-slab stride (doubles): room for the b-half shift
+  static constexpr int SHA = e4_pick_sa(K), SHB = e4_pick_sb(K);
+  static constexpr int P_DBL = K * SA + SHA + 8;
+  static constexpr int LDS_BYTES = (P_DBL + 8) * 8;
+  __device__ static constexpr int off(int a, int b) {
+    return a * SA + b * KP + (b >= KB ? SHB : 0) + (a >= KA ? SHA : 0);
+  }
+};
+
+template <int K>
+__device__ __forceinline__ void e4_stage_p(double* __restrict__ Ps, const double* __restrict__ p,
+                                           int tid) {
+  using EP = E4Plan<K>;
+  for (int idx = tid; idx < EP::K3; idx += E4_NT) {
+    const int a = idx / (K * K), b = (idx / K) % K;
+    Ps[EP::off(a, b) + idx % K] = p[idx];
+  }
+}
+
+// Lane (ha, hb): Y partials of its a-half over its b-half, Z partials of its b-half over its
+// a-half, W and d partials over its block; exchanged with two lane swaps (xor 1: a-halves,
+// xor 2: b-halves) in commutative, lane-symmetric order, so all lanes agree bitwise.
+template <int K>
+__device__ __forceinline__ double phase_a_e4(const double* __restrict__ Ps,
+                                             const double* __restrict__ ri,
+                                             const double* __restrict__ rj,
+                                             const double* __restrict__ rk, int ha, int hb,
+                                             double (&yv)[E4Plan<K>::KA],
+                                             double (&zc)[E4Plan<K>::KB], double (&wc)[K]) {
+  using EP = E4Plan<K>;
+  constexpr int KA = EP::KA, KB = EP::KB;
+  double ti[KA], tj[KB], tk[K];
+#pragma unroll
+  for (int s = 0; s < KA; ++s) ti[s] = (ha * KA + s < K) ? ri[ha * KA + s] : 0.0;
+#pragma unroll
+  for (int t = 0; t < KB; ++t) tj[t] = (hb * KB + t < K) ? rj[hb * KB + t] : 0.0;
+#pragma unroll
+  for (int g = 0; g < K; ++g) {
+    tk[g] = rk[g];
+    wc[g] = 0.0;
+  }
+#pragma unroll
+  for (int t = 0; t < KB; ++t) zc[t] = 0.0;
+  double dsum = 0.0;
+#pragma unroll
+  for (int s = 0; s < KA; ++s) {
+    const int a = ha * KA + s < K ? ha * KA + s : K - 1;
+    const double ta = ti[s];
+    double y = 0.0;
+#pragma unroll
+    for (int t = 0; t < KB; ++t) {
+      const int bb = hb * KB + t < K ? hb * KB + t : K - 1;
+      double pv[K];
+      lds_row<K>(pv, Ps + EP::off(a, bb));
+      double u = 0.0;
+#pragma unroll
+      for (int g = 0; g < K; ++g) u = fma(pv[g], tk[g], u);
+      y = fma(tj[t], u, y);
+      zc[t] = fma(ta, u, zc[t]);
+      const double tt = ta * tj[t];
+#pragma unroll
+      for (int g = 0; g < K; ++g) wc[g] = fma(tt, pv[g], wc[g]);
+    }
+    yv[s] = y;
     dsum = fma(ta, y, dsum);
   }
 #pragma unroll
+  for (int s = 0; s < KA; ++s) yv[s] += __shfl_xor(yv[s], 2, 64);
+#pragma unroll
+  for (int t = 0; t < KB; ++t) zc[t] += __shfl_xor(zc[t], 1, 64);
+#pragma unroll
   for (int g = 0; g < K; ++g) {
-    zc[g] += __shfl_xor(zc[g], 1, 64);
     wc[g] += __shfl_xor(wc[g], 1, 64);
+    wc[g] += __shfl_xor(wc[g], 2, 64);
   }
   dsum += __shfl_xor(dsum, 1, 64);
+  dsum += __shfl_xor(dsum, 2, 64);
   return dsum;
+}
+
+template <int K>
+__global__ __launch_bounds__(E4_NT, 4) void estep4_kernel(
+    const int4* __restrict__ obs, const int4* __restrict__ pos, const int* __restrict__ tile_r,
+    const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ contrib,
+    double* __restrict__ cvec, double* __restrict__ partL, int P, int R, long long n_obs_pad,
+    long long nnz, int ntiles, double eps, int ablate) {
+  using EP = E4Plan<K>;
+  constexpr int K3 = EP::K3, KA = EP::KA, KB = EP::KB;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Ps = smem;
+  double* scratch = smem + EP::P_DBL;
+  const int tid = threadIdx.x;
+  const int lo = tid >> 2, h = tid & 3, ha = h & 1, hb = h >> 1;
+  const int tile = blockIdx.x;
+  const int b = blockIdx.y;
+  const int r = __builtin_amdgcn_readfirstlane(tile_r[(tile * ET) / TILE]);
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+  const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
+  const size_t o = (size_t)tile * ET + lo;
+  const int4 e = obs[o];
+  const int4 q = pos[o];
+  const double n = (double)e.w;
+  e4_stage_p<K>(Ps, p, tid);
+  __syncthreads();
+  double yv[KA], zc[KB], wc[K], dsum = 1.0;
+  // ablate (measurement builds only, MMSBM_ABLATE): bit 0 skips phase A
+  if (!(ablate & 1))
+    dsum = phase_a_e4<K>(Ps, th + (size_t)e.x * K, th + (size_t)e.y * K, th + (size_t)e.z * K,
+                         ha, hb, yv, zc, wc);
+  const double d = dsum + eps;
+  const double c = n / d;
+  if (q.x >= 0 && !(ablate & 9)) {  // bit 3: skip the row stores (measurement only)
+    double* __restrict__ cb = contrib + (size_t)b * nnz * K;
+    if (hb == 0) {  // Y row, own a-half
+      double* ry = cb + (size_t)q.x * K + ha * KA;
+#pragma unroll
+      for (int s = 0; s < KA; ++s)
+        if (ha * KA + s < K) ry[s] = c * yv[s];
+    }
+    if (ha == 0) {  // Z row, own b-half
+      double* rz = cb + (size_t)q.y * K + hb * KB;
+#pragma unroll
+      for (int t = 0; t < KB; ++t)
+        if (hb * KB + t < K) rz[t] = c * zc[t];
+    } else {  // W row, g-half hb
+      double* rw = cb + (size_t)q.z * K;
+#pragma unroll
+      for (int g = 0; g < K; ++g)
+        if ((g >= KB) == (hb == 1)) rw[g] = c * wc[g];
+    }
+  }
+  if (h == 0) cvec[(size_t)b * n_obs_pad + o] = c;
+  const double ll = block_sum(h == 0 ? n * log(d) : 0.0, scratch);
+  if (tid == 0) partL[(size_t)b * ntiles + tile] = ll;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -381,57 +582,81 @@ __device__ __forceinline__ double phase_a_lds(const double* __restrict__ Ps,
 //   parameters, for free).
 // ------------------------------------------------------------------------------------------
 template <int K>
-__global__ __launch_bounds__((EPlan<K>::NT), (EPlan<K>::OCC)) void estep_kernel(
+__global__ __launch_bounds__((EPlan<K>::NT), (EPlan<K>::E_OCC)) void estep_kernel(
     const int4* __restrict__ obs, const int4* __restrict__ pos, const int* __restrict__ tile_r,
     const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ contrib,
     double* __restrict__ cvec, double* __restrict__ partL, int P, int R, long long n_obs_pad,
     long long nnz, int ntiles, double eps, int ablate) {
   using EP = EPlan<K>;
-  constexpr int K3 = EP::K3, H = EP::H, NT = EP::NT, KH = EP::KH;
+  constexpr int K3 = EP::K3, H = EP::H, NT = EP::NT, KH = EP::KH, NO = EP::NO;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* Ps = smem;
   double* scratch = smem + EP::P_DBL;
 
   const int tid = threadIdx.x;
-  const int lo = tid / H;  // observation within the tile
+  const int lo = tid / H;  // observation slot within the tile (x NO)
   const int h = tid % H;   // lane's share of the observation
   const int tile = blockIdx.x;
   const int b = blockIdx.y;
-  const int r = __builtin_amdgcn_readfirstlane(tile_r[(tile * ET) / TILE]);
+  const int r = __builtin_amdgcn_readfirstlane(tile_r[(tile * EP::EOBS) / TILE]);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-  const size_t o = (size_t)tile * ET + lo;
-  const int4 e = obs[o];
-  const int4 q = pos[o];  // CSR rows of slots 0, 1, 2 (-1 for padding)
-  const double n = (double)e.w;
   double* __restrict__ cb = contrib + (size_t)b * nnz * K;
   if constexpr (EP::STAGE_P) {
+    size_t o[NO];
+    int4 e[NO], q[NO];
+    const double* ri[NO];
+    const double* rj[NO];
+    const double* rk[NO];
+#pragma unroll
+    for (int m = 0; m < NO; ++m) {
+      o[m] = (size_t)tile * EP::EOBS + m * ET + lo;
+      e[m] = obs[o[m]];
+      q[m] = pos[o[m]];  // CSR rows of slots 0, 1, 2 (-1 for padding)
+      ri[m] = th + (size_t)e[m].x * K;
+      rj[m] = th + (size_t)e[m].y * K;
+      rk[m] = th + (size_t)e[m].z * K;
+    }
     stage_p<K>(Ps, p, tid, NT);
     __syncthreads();
-  }
-  double dsum = 1.0;
-  // ablate (measurement builds only, MMSBM_ABLATE): bit 0 skips phase A
-  if constexpr (EP::STAGE_P) {
-    double yv[KH], zc[K], wc[K];
-    if (!(ablate & 1))
-      dsum = phase_a_lds<K>(Ps, th + (size_t)e.x * K, th + (size_t)e.y * K, th + (size_t)e.z * K,
-                            h, yv, zc, wc);
-    const double d = dsum + eps;
-    const double c = n / d;
-    if (q.x >= 0 && !(ablate & 1)) {
-      double* ry = cb + (size_t)q.x * K + h * KH;
+    double yv[NO][KH], zc[NO][K], wc[NO][K], dsum[NO];
+    // ablate (measurement builds only, MMSBM_ABLATE): bit 0 skips phase A
+    if (!(ablate & 1)) {
+      phase_a_lds<K, NO>(Ps, ri, rj, rk, h, yv, zc, wc, dsum);
+    } else {
 #pragma unroll
-      for (int t = 0; t < KH; ++t)
-        if (h * KH + t < K) ry[t] = c * yv[t];
-      double* rzw = cb + (size_t)(h == 0 ? q.y : q.z) * K;
-#pragma unroll
-      for (int g = 0; g < K; ++g) rzw[g] = c * (h == 0 ? zc[g] : wc[g]);
+      for (int m = 0; m < NO; ++m) dsum[m] = 1.0;
     }
-    if (h == 0) cvec[(size_t)b * n_obs_pad + o] = c;
-    const double ll = block_sum(h == 0 ? n * log(d) : 0.0, scratch);
+    double llsum = 0.0;
+#pragma unroll
+    for (int m = 0; m < NO; ++m) {
+      const double n = (double)e[m].w;
+      const double d = dsum[m] + eps;
+      const double c = n / d;
+      if (q[m].x >= 0 && !(ablate & 1)) {
+        double* ry = cb + (size_t)q[m].x * K + h * KH;
+#pragma unroll
+        for (int t = 0; t < KH; ++t)
+          if (h * KH + t < K) ry[t] = c * yv[m][t];
+        double* rzw = cb + (size_t)(h == 0 ? q[m].y : q[m].z) * K;
+#pragma unroll
+        for (int g = 0; g < K; ++g) rzw[g] = c * (h == 0 ? zc[m][g] : wc[m][g]);
+      }
+      if (h == 0) {
+        cvec[(size_t)b * n_obs_pad + o[m]] = c;
+        llsum += n * log(d);
+      }
+    }
+    const double ll = block_sum(llsum, scratch);
     if (tid == 0) partL[(size_t)b * ntiles + tile] = ll;
   } else {
-    // scalar-p path: Y, Z, W land unscaled in the CSR rows, then are scaled in place
+    // scalar-p path (one lane per observation): Y, Z, W land unscaled in the CSR rows, then
+    // are scaled in place
+    const size_t o = (size_t)tile * ET + tid;
+    const int4 e = obs[o];
+    const int4 q = pos[o];
+    const double n = (double)e.w;
+    double dsum = 1.0;
     double* ry = cb + (size_t)(q.x >= 0 ? q.x : 0) * K;
     double* rz = cb + (size_t)(q.y >= 0 ? q.y : 0) * K;
     double* rw = cb + (size_t)(q.z >= 0 ? q.z : 0) * K;
@@ -453,90 +678,59 @@ __global__ __launch_bounds__((EPlan<K>::NT), (EPlan<K>::OCC)) void estep_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// M1, grid (G + theta_blocks, B), block 256.
-//  blocks [0, G): S accumulation (:1012 npr scatter, factorised):
+// M1 = S accumulation (:1012 npr scatter, factorised), grid (G, B), block 1024:
 //      S_r[a b g] = sum_obs c th_i[a] th_j[b] th_k[g]
-//    workgroup w owns a contiguous, balanced run of 64-observation tiles; each tile's
-//    c*theta_i / theta_j / theta_k rows are staged in LDS and consumed by a register-tiled
-//    outer product (lane = (a, b-chunk) cell block x link group).  Accumulators live in VGPRs
-//    across the whole run and are folded across link groups through LDS in a fixed order once
-//    per rating: G partial rows per rating instead of one per tile.
-//  blocks [G, ...): theta gather (:1016-1018) into theta_new, one wave per gene:
-//      theta_new[g][a] = theta[g][a] * (sum of the gene's contiguous c-scaled rows)[a] / deg[g]
-//    (sum over incidences in ascending CSR order per lane + fixed butterfly: reproducible)
-//    (theta itself is still read by the S blocks of this launch; M2 copies it back).
+// Workgroup w owns a contiguous, balanced run of 64-observation tiles (one workgroup per CU,
+// 16 waves: 4 per SIMD, which FP64 FMA needs).  The run is processed in windows of
+// rating-uniform tiles: the window's c*theta_i / theta_j / theta_k rows are staged in LDS at
+// once and consumed by a register-tiled outer product (lane = (a, b-chunk) cell block x link
+// group; a group strides the whole window, so its loop is long and balanced).  Accumulators
+// stay in VGPRs across windows and are folded across link groups through LDS in a fixed order
+// (up to RED_SLOTS partial copies per round) once per rating: G partial rows per rating.
 // ------------------------------------------------------------------------------------------
-constexpr int M1_NT = 256;
-constexpr int MT_BATCH = 4;  // theta gather: rows in flight per lane
+constexpr int M1_NT = 1024;
 
 template <int K>
 struct S1Plan {
-  using S = SPlan<K, M1_NT>;
+  // cell budget: accumulators + the staged theta_k row fit 128 VGPRs (4 waves/SIMD)
+  static constexpr int CELLS = (50 - 2 * K) < 40 ? ((50 - 2 * K) < K ? K : 50 - 2 * K) : 40;
+  using S = SPlan<K, M1_NT, CELLS>;
   static constexpr int K3 = K * K * K;
   static constexpr int KP = (K + 1) & ~1;
   static constexpr int RS = (KP % 4 == 2) ? KP : KP + 2;  // conflict-free 16-lane b128 rows
-  static constexpr int STAGE_DBL = 3 * ET * RS;
-  static constexpr int RED_SLOTS = S::LG / 2 < 2 ? S::LG / 2 : 2;
+  static constexpr int LDS_CAP = 144 * 1024;               // one workgroup per CU
+  // observations staged per window (multiple of ET): ~3/4 of the LDS
+  static constexpr int WOBS_RAW = (LDS_CAP * 3 / 4) / (3 * RS * 8 + 16) / ET * ET;
+  static constexpr int WOBS = WOBS_RAW > 8 * ET ? 8 * ET : (WOBS_RAW < ET ? ET : WOBS_RAW);
+  static constexpr int STAGE_DBL = 3 * WOBS * RS;
+  static constexpr int SLOTS_FIT = (LDS_CAP / 8 - 2 * WOBS) / K3;
+  static constexpr int RED_SLOTS_RAW = S::LG / 2 < SLOTS_FIT ? S::LG / 2 : SLOTS_FIT;
+  static constexpr int RED_SLOTS = S::LG < 2 ? 0 : (RED_SLOTS_RAW < 1 ? 1 : RED_SLOTS_RAW);
   static constexpr int RED_DBL = RED_SLOTS * K3;
-  static constexpr int LDS_BYTES = (STAGE_DBL > RED_DBL ? STAGE_DBL : RED_DBL) * 8;
-  static_assert(LDS_BYTES <= LDS_BUDGET, "M1 LDS plan over budget");
+  static constexpr int BODY_DBL = ((STAGE_DBL > RED_DBL ? STAGE_DBL : RED_DBL) + 1) & ~1;
+  static constexpr int WREC_DBL = WOBS + (3 * WOBS + 1) / 2;  // c (double) + 3 gene ids (int)
+  static constexpr int LDS_BYTES = (BODY_DBL + WREC_DBL) * 8;
+  static_assert(LDS_BYTES <= LDS_CAP + 16 * 1024, "M1 LDS plan over budget");
 };
 
 template <int K>
-__global__ __launch_bounds__(M1_NT, 3) void m1_kernel(
+__global__ __launch_bounds__(M1_NT) void m1_kernel(
     const int4* __restrict__ obs, const int* __restrict__ tile_r, const double* __restrict__ theta,
-    double* __restrict__ theta_new, const double* __restrict__ contrib,
-    const double* __restrict__ cvec, const int* __restrict__ gptr, const int* __restrict__ deg,
-    double* __restrict__ partS, int P, int R, long long n_obs_pad, long long nnz, int G,
-    int ablate) {
-  using SP = typename S1Plan<K>::S;
+    const double* __restrict__ cvec, double* __restrict__ partS, int P, int R,
+    long long n_obs_pad, int G, int ablate) {
   using PL = S1Plan<K>;
-  constexpr int K3 = PL::K3, RS = PL::RS;
+  using SP = typename PL::S;
+  constexpr int K3 = PL::K3, RS = PL::RS, WOBS = PL::WOBS;
   constexpr int NB = SP::NB, NBC = SP::NBC, NBLK = SP::NBLK, LG = SP::LG;
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
   const double* __restrict__ th = theta + (size_t)b * P * K;
-
-  if ((int)blockIdx.x >= G) {  // ---------------------------------------------- theta gather
-    const int g = ((int)blockIdx.x - G) * 4 + (tid >> 6);
-    const int lane = tid & 63;
-    if (g >= P) return;  // wave-uniform
-    // the gene's c-scaled rows are contiguous: rows q0..q1-1, one row (K doubles) per lane
-    const double* __restrict__ cb = contrib + (size_t)b * nnz * K;
-    double acc[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    const int q0 = gptr[g], q1 = gptr[g + 1];
-    for (int qb = q0; qb < q1; qb += 64 * MT_BATCH) {
-      double row[MT_BATCH][K];
-#pragma unroll
-      for (int j = 0; j < MT_BATCH; ++j) {
-        const int qq = qb + j * 64 + lane;
-        const double* __restrict__ src = cb + (size_t)(qq < q1 ? qq : q0) * K;
-#pragma unroll
-        for (int k = 0; k < K; ++k) row[j][k] = qq < q1 ? src[k] : 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < MT_BATCH; ++j)
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc[k] += row[j][k];
-    }
-    double mine = 0.0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double t = wave_sum(acc[k]);
-      if (lane == k) mine = t;
-    }
-    if (lane < K)
-      theta_new[(size_t)b * P * K + (size_t)g * K + lane] = th[(size_t)g * K + lane] * mine / (double)deg[g];
-    return;
-  }
-
-  // -------------------------------------------------------------------- S accumulation
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* As = smem;  // c * theta_i rows
-  double* Bs = As + ET * RS;
-  double* Gs = Bs + ET * RS;
+  double* As = smem;  // [WOBS][RS] c * theta_i
+  double* Bs = As + WOBS * RS;
+  double* Gs = Bs + WOBS * RS;
+  double* Wc = smem + PL::BODY_DBL;
+  int* Wg = reinterpret_cast<int*>(Wc + WOBS);
   const int w = blockIdx.x;
   const int T = (int)(n_obs_pad / ET);
   const int t0 = (int)((long long)w * T / G), t1 = (int)((long long)(w + 1) * T / G);
@@ -605,28 +799,41 @@ __global__ __launch_bounds__(M1_NT, 3) void m1_kernel(
     };
 
     int cur_r = tile_r[(t0 * ET) / TILE];
-    for (int t = t0; t < t1; ++t) {
+    int t = t0;
+    while (t < t1) {
+      // window: up to WOBS/ET tiles of one rating
       const int rt = tile_r[(t * ET) / TILE];
       if (rt != cur_r) {  // workgroup-uniform
         flush(cur_r);
         cur_r = rt;
       }
-      __syncthreads();  // previous tile's readers are done with the stage
-      if (tid < 3 * ET) {
-        const int l = tid % ET, which = tid / ET;
-        const size_t oo = (size_t)t * ET + l;
+      int tw = t + 1;
+      while (tw < t1 && tw - t < WOBS / ET && tile_r[(tw * ET) / TILE] == rt) ++tw;
+      const int nobs = (tw - t) * ET;
+      __syncthreads();  // previous window's readers are done with the stage / records
+#pragma unroll 1
+      for (int idx = tid; idx < nobs; idx += M1_NT) {
+        const size_t oo = (size_t)t * ET + idx;
         const int4 e = obs[oo];
-        const int gene = which == 0 ? e.x : which == 1 ? e.y : e.z;
-        const double sc = which == 0 ? cvec[(size_t)b * n_obs_pad + oo] : 1.0;
-        const double* __restrict__ src = th + (size_t)gene * K;
-        double* dst = smem + which * ET * RS + l * RS;
+        Wg[idx * 3 + 0] = e.x;
+        Wg[idx * 3 + 1] = e.y;
+        Wg[idx * 3 + 2] = e.z;
+        Wc[idx] = cvec[(size_t)b * n_obs_pad + oo];
+      }
+      __syncthreads();
+#pragma unroll 1
+      for (int idx = tid; idx < 3 * nobs; idx += M1_NT) {  // gather the window's theta rows
+        const int l = idx % nobs, slot = idx / nobs;
+        const double sc = slot == 0 ? Wc[l] : 1.0;
+        const double* __restrict__ src = th + (size_t)Wg[l * 3 + slot] * K;
+        double* dst = smem + (size_t)slot * WOBS * RS + l * RS;
 #pragma unroll
         for (int g = 0; g < K; ++g) dst[g] = sc * src[g];
       }
       __syncthreads();
       if (active) {
 #pragma unroll 1
-        for (int l = grp; l < ET; l += LG) {
+        for (int l = grp; l < nobs; l += LG) {
           const double av = As[l * RS + alpha];
           double gv[K];
           lds_row<K>(gv, Gs + l * RS);
@@ -640,6 +847,7 @@ __global__ __launch_bounds__(M1_NT, 3) void m1_kernel(
           }
         }
       }
+      t = tw;
     }
     flush(cur_r);
   }
@@ -655,27 +863,62 @@ __global__ void csr_invert_kernel(const int* __restrict__ ginc, long long nnz, i
 }
 
 // ------------------------------------------------------------------------------------------
-// M2, grid (ceil(K3 / 4) + copy_blocks, B), block 256.
+// M2, grid (ceil(K3 / 4) + theta_blocks, B), block 256.
 //  blocks [0, p_blocks): p (:1021-1028), one wave per cell: S_r = sum over the G partial
 //    rows (lane-strided, fixed butterfly); npr_r = p_r S_r; p_r <- npr_r / (eps + sum_r npr_r).
-//  blocks [p_blocks, ...): theta <- theta_new.
+//  blocks [p_blocks, ...): theta (:1016-1018), in place, one wave per gene:
+//      theta[g][a] <- theta[g][a] * (sum of the gene's contiguous c-scaled rows)[a] / deg[g]
+//    (rows in ascending CSR order per lane + fixed butterfly: reproducible).
 // ------------------------------------------------------------------------------------------
+constexpr int MT_BATCH = 4;  // theta gather: rows in flight per lane
+
 template <int K>
-__global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr,
-                                                 double* __restrict__ theta,
-                                                 const double* __restrict__ theta_new,
-                                                 const double* __restrict__ partS, int P, int R,
-                                                 int G, int p_blocks, double eps) {
+__global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double* __restrict__ theta,
+                                                 const double* __restrict__ partS,
+                                                 const double* __restrict__ contrib,
+                                                 const int* __restrict__ gptr,
+                                                 const int* __restrict__ deg, int P, int R, int G,
+                                                 long long nnz, int p_blocks, double eps,
+                                                 int ablate) {
   constexpr int K3 = K * K * K;
   const int b = blockIdx.y;
-  if ((int)blockIdx.x >= p_blocks) {
-    const size_t n = (size_t)P * K;
-    const size_t i = ((size_t)blockIdx.x - p_blocks) * 256 + threadIdx.x;
-    if (i < n) theta[(size_t)b * n + i] = theta_new[(size_t)b * n + i];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  if ((int)blockIdx.x >= p_blocks) {  // --------------------------------------------- theta
+    const int g = ((int)blockIdx.x - p_blocks) * 4 + (tid >> 6);
+    if (g >= P || (ablate & 4)) return;  // wave-uniform
+    const double* __restrict__ cb = contrib + (size_t)b * nnz * K;
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    const int q0 = gptr[g], q1 = gptr[g + 1];
+    for (int qb = q0; qb < q1; qb += 64 * MT_BATCH) {
+      double row[MT_BATCH][K];
+#pragma unroll
+      for (int j = 0; j < MT_BATCH; ++j) {
+        const int qq = qb + j * 64 + lane;
+        const double* __restrict__ src = cb + (size_t)(qq < q1 ? qq : q0) * K;
+#pragma unroll
+        for (int k = 0; k < K; ++k) row[j][k] = qq < q1 ? src[k] : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < MT_BATCH; ++j)
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] += row[j][k];
+    }
+    double mine = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double t = wave_sum(acc[k]);
+      if (lane == k) mine = t;
+    }
+    if (lane < K) {
+      double* row = theta + (size_t)b * P * K + (size_t)g * K;
+      row[lane] = row[lane] * mine / (double)deg[g];
+    }
     return;
   }
-  const int cell = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+  const int cell = blockIdx.x * 4 + (tid >> 6);  // ------------------------------------- p
   if (cell >= K3) return;  // wave-uniform
   const double* __restrict__ rows = partS + (size_t)b * G * R * K3 + cell;
   double npr[MAX_R];
@@ -838,7 +1081,6 @@ struct mmsbm_ctx {
   double* cvec = nullptr;
   double* partS = nullptr;
   double* partL = nullptr;
-  double* theta_new = nullptr;
   // current iterate (only valid during a call)
   double* theta_mut = nullptr;
   double* pr_mut = nullptr;
@@ -847,6 +1089,7 @@ struct mmsbm_ctx {
   int timing_stride = 1;  // time every n-th iteration
   int ablate = 0;  // MMSBM_ABLATE (measurement only)
   int sacc_wgs = SACC_WGS;  // S-accumulation workgroups requested (MMSBM_SACC_WGS)
+  int estep_variant = 0;    // 0: four lanes per observation where compiled; 1: two (MMSBM_ESTEP)
   std::vector<hipEvent_t> ev[3];  // start/stop pairs per kernel id (E, M1, M2)
   size_t nev[3] = {0, 0, 0};
 };
@@ -854,7 +1097,7 @@ struct mmsbm_ctx {
 namespace {
 
 struct WsLayout {
-  size_t contrib, cvec, partS, partL, theta_new, total;
+  size_t contrib, cvec, partS, partL, total;
 };
 
 // S-accumulation workgroups actually launched: never more than the train set's tiles.
@@ -880,8 +1123,6 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   L.partL = off;  // one log-likelihood partial per 64-observation tile of either set
   long long nt = (tr.n_obs_pad > te.n_obs_pad ? tr.n_obs_pad : te.n_obs_pad) / ET;
   off += align_up((size_t)c->B * (nt > 0 ? nt : 1) * sizeof(double));
-  L.theta_new = off;
-  off += align_up((size_t)c->B * c->P * c->K * sizeof(double));
   L.total = off;
   return L;
 }
@@ -891,7 +1132,18 @@ int launch_estep(mmsbm_ctx* c, hipStream_t s) {
   using EP = EPlan<K>;
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
   if (tr.ntiles == 0) return MMSBM_OK;
-  const int nt = (int)(tr.n_obs_pad / ET);
+  if constexpr (E4Plan<K>::ON) {
+    if (c->estep_variant == 0) {
+      const int nt = (int)(tr.n_obs_pad / ET);
+      estep4_kernel<K><<<dim3(nt, c->B), E4_NT, E4Plan<K>::LDS_BYTES, s>>>(
+          tr.obs, reinterpret_cast<const int4*>(c->pos), tr.tile_r, c->theta_mut, c->pr_mut,
+          c->contrib, c->cvec, c->partL, c->P, c->R, tr.n_obs_pad, c->nnz, nt, c->eps,
+          c->ablate);
+      HIP_TRY(hipGetLastError());
+      return MMSBM_OK;
+    }
+  }
+  const int nt = (int)(tr.n_obs_pad / EP::EOBS);
   estep_kernel<K><<<dim3(nt, c->B), EP::NT, EP::LDS_BYTES, s>>>(
       tr.obs, reinterpret_cast<const int4*>(c->pos), tr.tile_r, c->theta_mut, c->pr_mut,
       c->contrib, c->cvec, c->partL, c->P, c->R, tr.n_obs_pad, c->nnz, nt, c->eps, c->ablate);
@@ -904,10 +1156,14 @@ int launch_m1(mmsbm_ctx* c, hipStream_t s) {
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
   if (tr.ntiles == 0) return MMSBM_OK;
   const int G = sacc_groups(c);
-  const int theta_blocks = (c->P + 3) / 4;
-  m1_kernel<K><<<dim3(G + theta_blocks, c->B), M1_NT, S1Plan<K>::LDS_BYTES, s>>>(
-      tr.obs, tr.tile_r, c->theta_mut, c->theta_new, c->contrib, c->cvec, c->gptr, c->deg,
-      c->partS, c->P, c->R, tr.n_obs_pad, c->nnz, G, c->ablate);
+  static bool attr = false;  // LDS above 64 KB needs the opt-in once per kernel
+  if (!attr) {
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&m1_kernel<K>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, S1Plan<K>::LDS_BYTES));
+    attr = true;
+  }
+  m1_kernel<K><<<dim3(G, c->B), M1_NT, S1Plan<K>::LDS_BYTES, s>>>(
+      tr.obs, tr.tile_r, c->theta_mut, c->cvec, c->partS, c->P, c->R, tr.n_obs_pad, G, c->ablate);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -918,10 +1174,10 @@ int launch_m2(mmsbm_ctx* c, hipStream_t s) {
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
   if (tr.ntiles == 0) return MMSBM_OK;
   const int p_blocks = (K3 + 3) / 4;
-  const int copy_blocks = (int)(((long long)c->P * K + 255) / 256);
-  m2_kernel<K><<<dim3(p_blocks + copy_blocks, c->B), 256, 0, s>>>(
-      c->pr_mut, c->theta_mut, c->theta_new, c->partS, c->P, c->R, sacc_groups(c), p_blocks,
-      c->eps);
+  const int theta_blocks = (c->P + 3) / 4;
+  m2_kernel<K><<<dim3(p_blocks + theta_blocks, c->B), 256, 0, s>>>(
+      c->pr_mut, c->theta_mut, c->partS, c->contrib, c->gptr, c->deg, c->P, c->R, sacc_groups(c),
+      c->nnz, p_blocks, c->eps, c->ablate);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -993,6 +1249,7 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   auto* c = new mmsbm_ctx();
   c->device = device;
   if (const char* ab = getenv("MMSBM_ABLATE")) c->ablate = atoi(ab);
+  if (const char* v = getenv("MMSBM_ESTEP")) c->estep_variant = atoi(v);
   if (const char* t = getenv("MMSBM_SACC_WGS")) {
     const int v = atoi(t);
     if (v >= 1) c->sacc_wgs = v;
@@ -1129,7 +1386,6 @@ int mmsbm_set_workspace(mmsbm_ctx* c, void* ws, int64_t bytes) {
   c->cvec = (double*)(c->ws + L.cvec);
   c->partS = (double*)(c->ws + L.partS);
   c->partL = (double*)(c->ws + L.partL);
-  c->theta_new = (double*)(c->ws + L.theta_new);
   return MMSBM_OK;
 }
 
