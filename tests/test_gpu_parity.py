@@ -135,9 +135,10 @@ def test_s_accumulation_workgroup_splits(tmp_path, monkeypatch, K, groups):
 
 
 def test_estep_variants_agree(tmp_path, monkeypatch):
-    """The two E-step kernels (4-lane default, MMSBM_ESTEP=1) both match the oracle."""
+    """The E-step variants (fused MFMA default, 2-lane VALU + M1, 4-lane VALU + M1) all match
+    the oracle."""
     tr, te = _fold(tmp_path, 400, 8000, seed=21, multi_frac=0.05)
-    for variant in ("0", "1"):
+    for variant in ("0", "1", "2"):
         monkeypatch.setenv("MMSBM_ESTEP", variant)
         m = _gpu_model(tr, te)
         random.seed(3)

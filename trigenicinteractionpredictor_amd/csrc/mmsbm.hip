@@ -33,6 +33,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <cstdarg>
 #include <cstdint>
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(E4_NT, 4) void estep4_kernel(
   const double d = dsum + eps;
   const double c = n / d;
   if (q.x >= 0 && !(ablate & 9)) {  // bit 3: skip the row stores (measurement only)
-    double* __restrict__ cb = contrib + (size_t)b * nnz * K;
+    double* __restrict__ cb = contrib + (size_t)b * (nnz + 1) * K;
     if (hb == 0) {  // Y row, own a-half
       double* ry = cb + (size_t)q.x * K + ha * KA;
 #pragma unroll
@@ -601,7 +602,7 @@ __global__ __launch_bounds__((EPlan<K>::NT), (EPlan<K>::E_OCC)) void estep_kerne
   const int r = __builtin_amdgcn_readfirstlane(tile_r[(tile * EP::EOBS) / TILE]);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-  double* __restrict__ cb = contrib + (size_t)b * nnz * K;
+  double* __restrict__ cb = contrib + (size_t)b * (nnz + 1) * K;
   if constexpr (EP::STAGE_P) {
     size_t o[NO];
     int4 e[NO], q[NO];
@@ -863,23 +864,364 @@ __global__ void csr_invert_kernel(const int* __restrict__ ginc, long long nnz, i
 }
 
 // ------------------------------------------------------------------------------------------
-// M2, grid (ceil(K3 / 4) + theta_blocks, B), block 256.
-//  blocks [0, p_blocks): p (:1021-1028), one wave per cell: S_r = sum over the G partial
-//    rows (lane-strided, fixed butterfly); npr_r = p_r S_r; p_r <- npr_r / (eps + sum_r npr_r).
+// Which S-partial rows hold rating r (M2's view of partS):
+//   row(b, w, r) = partS + ((b * G + w) * rs + r * ro) * K3,  w in [wlo[r], whi[r])
+//   M1 layout: every workgroup writes every rating (rs = R, ro = 1, w in [0, G));
+//   fused MFMA layout: a workgroup owns one rating (rs = 1, ro = 0, w in that rating's range).
+// The fused kernel also reads grp[r] = first 16-observation group of rating r.
+// ------------------------------------------------------------------------------------------
+struct SRows {
+  int wlo[MAX_R], whi[MAX_R];
+  int grp[MAX_R + 1];
+  int rs, ro;
+};
+
+// ------------------------------------------------------------------------------------------
+// Fused E-step + S accumulation on FP64 MFMA (:987-1012), grid (G, B), block 64 * NW.
+//
+// v_mfma_f64_4x4x4f64 computes four independent 4x4x4 products ("blocks") per wave; with
+// lane = 16 * hi + 4 * blk + lo its operands are A[blk][m = lo][k = hi], B[blk][k = hi][n = lo]
+// and its result D[blk][m = hi][n = lo] (probed: tools/micro/mfma_layout.hip).  A wave takes
+// 16 observations at a time (a "group"); observation oA = lane & 15 feeds the A side, the
+// result rows belong to observation oD = 4 * blk + hi.
+//   U-phase   U[o][a][b] = sum_g p_r[a][b][g] th_k[o][g]: per (a, b-block) tile 1 MFMA per
+//             g-block (A = th_k of oA, B = p_r from LDS, the same in all four blocks).  Lane
+//             (oD, lo) keeps b = 4 bb + lo, so Z[b] = sum_a th_i[a] U[a][b] is complete in the
+//             lane and Y[a] = sum_b th_j[b] U[a][b] needs one quad butterfly.
+//             d = eps + sum_a th_i[a] Y[a], c = n / d.
+//   KR        c th_i[a] th_j[b] of the group's observations written to a per-wave LDS image.
+//   W-phase   W'[o][g] = sum_(a,b) KR[o][(a,b)] p_r[a][b][g] (= c W): k over the K^2 cells.
+//   S-phase   S[(a,b)][g] += sum_o KR[o][(a,b)] th_k[o][g]: k over the group's observations,
+//             accumulators stay in registers across all the wave's groups.
+// Contributions c Y, c Z, c W go to the observation's three gene-CSR rows (M2 multiplies by
+// theta and divides by deg).  At the end the NW waves' S accumulators are summed in LDS in a
+// fixed order: one partial S row per workgroup (each workgroup owns one rating).  Every sum
+// has a fixed order: bitwise reproducible.
+// ------------------------------------------------------------------------------------------
+constexpr int XG = 16;  // observations per wave group
+
+template <int K>
+struct XPlan {
+  static constexpr int NG = (K + 3) / 4;      // 4-wide blocks of a / b / g
+  static constexpr int KP = 4 * NG;
+  static constexpr int K2 = K * K, K3 = K * K * K;
+  static constexpr int NC = (K2 + 3) / 4;     // W-phase k-steps over the (a, b) cells
+  static constexpr int KRW = 4 * NC;          // KR cells per observation (zero padded)
+  static constexpr int KRS = KRW + 2;         // row stride = 2 (mod 4): conflict-free W reads
+  static constexpr int NT4 = (K2 + 15) / 16;  // S-phase 16-cell tiles
+  static constexpr int SACC = NT4 * NG;       // S accumulators per lane
+  static constexpr int P_DBL = K * KP * KP;   // p_r image [a][b][g], b and g zero padded
+  static constexpr int IMG = 3 * XG * KP;     // th_i / th_j / th_k rows of the wave's group
+  static constexpr int WAVE_DBL = XG * KRS + IMG;
+  static constexpr int NW = (P_DBL + 8 * WAVE_DBL + 8) * 8 <= 160 * 1024 ? 8 : 4;
+  static constexpr int NT = 64 * NW;
+  static constexpr int LDS_BYTES = (P_DBL + NW * WAVE_DBL + 8) * 8;
+  static constexpr bool ON = K >= 2 && K <= 12;
+  static_assert(!ON || SACC * 64 <= WAVE_DBL, "S reduction must fit the wave images");
+  static_assert(!ON || LDS_BYTES <= 160 * 1024, "fused E-step LDS plan over budget");
+};
+
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// v within a quad of lanes, permuted by the DPP quad_perm CTRL (0xB1: xor 1, 0x4E: xor 2).
+template <int CTRL>
+__device__ __forceinline__ double quad_perm(double v) {
+  const long long x = __double_as_longlong(v);
+  const int l = __builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+  const int h = __builtin_amdgcn_mov_dpp((int)(x >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)h << 32) | (unsigned int)l);
+}
+
+// LDS writes of this wave visible to its own later reads (no workgroup barrier; a wave's LDS
+// operations execute in order, the fence only keeps the compiler from reordering them).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Optional per-wave phase clock (MMSBM_TRACE, measurement only): [wave][16] cycle sums.
+struct XTrace {
+  unsigned long long* out;
+  __device__ __forceinline__ unsigned long long now() const { return out ? clock64() : 0ull; }
+};
+
+template <int K>
+__global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
+    const int4* __restrict__ obs, const int4* __restrict__ pos, const double* __restrict__ theta,
+    const double* __restrict__ pr, double* __restrict__ contrib, double* __restrict__ partS,
+    double* __restrict__ partL, SRows rg, int P, int R, long long nnz, int G, double eps,
+    XTrace tr) {
+  using X = XPlan<K>;
+  constexpr int NG = X::NG, KP = X::KP, K2 = X::K2, K3 = X::K3, NC = X::NC, NT4 = X::NT4;
+  constexpr int KRS = X::KRS, KRW = X::KRW, NW = X::NW, NT = X::NT, SACC = X::SACC;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Pl = smem;  // [K][KP][KP]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* KR = smem + X::P_DBL + wv * X::WAVE_DBL;  // [XG][KRS]
+  double* TI = KR + XG * KRS;                        // [XG][KP] th_i of the group's observations
+  double* TJ = TI + XG * KP;
+  double* TK = TJ + XG * KP;
+  double* scratch = smem + X::P_DBL + NW * X::WAVE_DBL;
+  const int hi = lane >> 4, lo = lane & 3;
+  const int oA = lane & 15, oD = 4 * ((lane >> 2) & 3) + hi;
+  const int w = blockIdx.x, b = blockIdx.y;
+  unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long t_start = tr.now();
+  int r = 0;
+  while (r + 1 < R && w >= rg.whi[r]) ++r;  // workgroup-uniform
+  const int nwg = rg.whi[r] - rg.wlo[r], lw = w - rg.wlo[r];
+  const int ng = rg.grp[r + 1] - rg.grp[r];
+  const int g0 = rg.grp[r] + (int)((long long)lw * ng / nwg);
+  const int g1 = rg.grp[r] + (int)((long long)(lw + 1) * ng / nwg);
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+  const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
+  double* __restrict__ cb = contrib + (size_t)b * (nnz + 1) * K;
+
+  // the first group's records and theta values are in flight while p_r is staged
+  int grp = g0 + wv;
+  int4 eA = make_int4(0, 0, 0, 0), eD = eA, qD = eA, nA = eA, nD = eA, nQ = eA;
+  double aU[NG], tjD[NG], tiD4[NG];  // th_k[oA][4s+hi], th_j[oD][4j+lo], th_i[oD][4j+lo]
+  auto load_theta = [&](const int4& a, const int4& d, double (&u)[NG], double (&tj)[NG],
+                        double (&ti)[NG]) {
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      const int g = 4 * s + hi, v = 4 * s + lo;
+      u[s] = g < K ? th[(size_t)a.z * K + g] : 0.0;
+      tj[s] = v < K ? th[(size_t)d.y * K + v] : 0.0;
+      ti[s] = v < K ? th[(size_t)d.x * K + v] : 0.0;
+    }
+  };
+  if (grp < g1) {
+    const size_t r0 = (size_t)grp * XG;
+    eA = obs[r0 + oA];
+    eD = obs[r0 + oD];
+    qD = pos[r0 + oD];
+    load_theta(eA, eD, aU, tjD, tiD4);
+  }
+
+  for (int idx = tid; idx < X::P_DBL; idx += NT) {
+    const int g = idx % KP, bq = (idx / KP) % KP, a = idx / (KP * KP);
+    Pl[idx] = (g < K && bq < K) ? p[(a * K + bq) * K + g] : 0.0;
+  }
+  if constexpr (KRW > K2) {  // pad cells of the W-phase k-steps stay 0
+    for (int idx = lane; idx < XG * (KRW - K2); idx += 64)
+      KR[(idx / (KRW - K2)) * KRS + K2 + idx % (KRW - K2)] = 0.0;
+  }
+  __syncthreads();
+  unsigned long long t0 = tr.now();
+  tph[0] = t0 - t_start;
+
+  double sacc[NT4][NG];
+#pragma unroll
+  for (int t = 0; t < NT4; ++t)
+#pragma unroll
+    for (int u = 0; u < NG; ++u) sacc[t][u] = 0.0;
+  int ngrp = 0;
+
+  while (grp < g1) {
+    ++ngrp;
+    // ---- theta images of this group (LDS), then prefetch the next group
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      TK[oA * KP + 4 * s + hi] = aU[s];
+      TJ[oD * KP + 4 * s + lo] = tjD[s];
+      TI[oD * KP + 4 * s + lo] = tiD4[s];
+    }
+    const int gn = grp + NW;
+    {  // records of the next group (its theta values are fetched after the U-phase); past the
+       // end the current group is re-read (branch-free, unused)
+      const size_t r1 = (size_t)(gn < g1 ? gn : grp) * XG;
+      nA = obs[r1 + oA];
+      nD = obs[r1 + oD];
+      nQ = pos[r1 + oD];
+    }
+    wave_lds_sync();
+
+    // ---- U-phase: per a, NG x NG MFMAs with the NG (b-block) accumulators innermost
+    double yp[K], zp[NG];
+#pragma unroll
+    for (int bb = 0; bb < NG; ++bb) zp[bb] = 0.0;
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+      double bf[NG][NG];
+#pragma unroll
+      for (int bb = 0; bb < NG; ++bb)
+#pragma unroll
+        for (int s = 0; s < NG; ++s) bf[bb][s] = Pl[(a * KP + 4 * bb + lo) * KP + 4 * s + hi];
+      double acc[NG];
+#pragma unroll
+      for (int bb = 0; bb < NG; ++bb) acc[bb] = 0.0;
+#pragma unroll
+      for (int s = 0; s < NG; ++s)
+#pragma unroll
+        for (int bb = 0; bb < NG; ++bb) acc[bb] = mfma4(aU[s], bf[bb][s], acc[bb]);
+      const double ta = TI[oD * KP + a];
+      double y = 0.0;
+#pragma unroll
+      for (int bb = 0; bb < NG; ++bb) {
+        y = fma(tjD[bb], acc[bb], y);
+        zp[bb] = fma(ta, acc[bb], zp[bb]);
+      }
+      yp[a] = y;
+    }
+    unsigned long long t1 = tr.now();
+    tph[1] += t1 - t0;
+    // theta values of the next group: in flight through the rest of this one
+    double aU2[NG], tjD2[NG], tiD42[NG];
+    load_theta(nA, nD, aU2, tjD2, tiD42);
+    // d = eps + sum_b th_j[b] Z[b]: this lane's three b, then the quad
+    double dsum = 0.0;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) dsum = fma(tjD[j], zp[j], dsum);
+    dsum += quad_perm<0xB1>(dsum);
+    dsum += quad_perm<0x4E>(dsum);
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+      yp[a] += quad_perm<0xB1>(yp[a]);
+      yp[a] += quad_perm<0x4E>(yp[a]);
+    }
+    const double c = (double)eD.w / (dsum + eps);
+
+    // ---- KR image: c th_i[a] th_j[b] for observation oA, a = hi + 4 j
+    const double cA = __shfl(c, 16 * (oA & 3) + 4 * (oA >> 2), 64);
+    double tj[K];
+#pragma unroll
+    for (int bq = 0; bq < K; ++bq) tj[bq] = TJ[oA * KP + bq];
+    double* KRo = KR + oA * KRS;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const int a = hi + 4 * j;
+      if (a < K) {
+        const double ct = cA * TI[oA * KP + a];
+#pragma unroll
+        for (int bq = 0; bq < K; ++bq) KRo[a * K + bq] = ct * tj[bq];
+      }
+    }
+    wave_lds_sync();
+    unsigned long long t2 = tr.now();
+    tph[2] += t2 - t1;
+
+    // ---- W-phase: W' = c W for observation oD, g = 4 u + lo
+    double wacc[NG];
+#pragma unroll
+    for (int u = 0; u < NG; ++u) wacc[u] = 0.0;
+#pragma unroll
+    for (int s = 0; s < NC; ++s) {
+      const int cell = 4 * s + hi;
+      const int cc = cell < K2 ? cell : K2 - 1;
+      const double av = KRo[cell];
+      const double* pb = Pl + ((cc / K) * KP + cc % K) * KP + lo;
+#pragma unroll
+      for (int u = 0; u < NG; ++u) wacc[u] = mfma4(av, pb[4 * u], wacc[u]);
+    }
+    unsigned long long t3 = tr.now();
+    tph[3] += t3 - t2;
+
+    // ---- contributions of observation oD: entries 4 j + lo of its three gene-CSR rows
+    {
+      const bool real = qD.x >= 0;  // padding observations write the trash row (nnz)
+      double* ri = cb + (size_t)(real ? qD.x : nnz) * K;
+      double* rj = cb + (size_t)(real ? qD.y : nnz) * K;
+      double* rk = cb + (size_t)(real ? qD.z : nnz) * K;
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        const int v = 4 * j + lo;
+        const int vs = v < K ? v : K - 1;  // the ragged block's extra lanes repeat entry K-1
+        double y = yp[4 * j];
+#pragma unroll
+        for (int t = 1; t < 4; ++t)
+          if (4 * j + t < K && lo == t) y = yp[4 * j + t];
+        double* trash = cb + (size_t)nnz * K;
+        (v < K ? ri : trash)[vs] = c * y;
+        (v < K ? rj : trash)[vs] = c * zp[j];
+        (v < K ? rk : trash)[vs] = wacc[j];
+      }
+    }
+    unsigned long long t4 = tr.now();
+    tph[4] += t4 - t3;
+
+    // ---- S-phase: k over the group's observations o = 4 s + hi
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int o = 4 * s + hi;
+      double bS[NG];
+#pragma unroll
+      for (int u = 0; u < NG; ++u) bS[u] = TK[o * KP + 4 * u + lo];
+      const double* KRs = KR + o * KRS;
+#pragma unroll
+      for (int t = 0; t < NT4; ++t) {
+        const int cell = 16 * t + oA;
+        const double av = KRs[cell < KRW ? cell : 0];  // cells >= K2 feed discarded S entries
+#pragma unroll
+        for (int u = 0; u < NG; ++u) sacc[t][u] = mfma4(av, bS[u], sacc[t][u]);
+      }
+    }
+    wave_lds_sync();  // this group's image reads complete before the next group's writes
+    t0 = tr.now();
+    tph[5] += t0 - t4;
+
+    eA = nA;
+    eD = nD;
+    qD = nQ;
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      aU[s] = aU2[s];
+      tjD[s] = tjD2[s];
+      tiD4[s] = tiD42[s];
+    }
+    grp = gn;
+  }
+
+  __syncthreads();
+  double* red = smem + X::P_DBL;  // [NW][SACC][64] over the wave images
+#pragma unroll
+  for (int t = 0; t < NT4; ++t)
+#pragma unroll
+    for (int u = 0; u < NG; ++u) red[(wv * SACC + t * NG + u) * 64 + lane] = sacc[t][u];
+  __syncthreads();
+  double* __restrict__ rowS = partS + ((size_t)b * G + w) * K3;
+  for (int idx = tid; idx < SACC * 64; idx += NT) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += red[q * SACC * 64 + idx];
+    const int t = idx >> 6, ln = idx & 63;
+    const int cell = 16 * (t / NG) + 4 * ((ln >> 2) & 3) + (ln >> 4);
+    const int g = 4 * (t % NG) + (ln & 3);
+    if (cell < K2 && g < K) rowS[cell * K + g] = s;
+  }
+  if (tr.out && lane == 0) {
+    const unsigned long long t_end = tr.now();
+    unsigned long long* o = tr.out + ((size_t)(b * gridDim.x + w) * NW + wv) * 16;
+    for (int q = 0; q < 6; ++q) o[q] = tph[q];
+    o[6] = t_end - t0;
+    o[7] = (unsigned long long)ngrp;
+    o[8] = t_end - t_start;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// M2, grid (p_blocks + theta_blocks, B), block 256.
+//  blocks [0, p_blocks): p (:1021-1028), 8 cells x 32 row slices per block: S_r = sum of the
+//    rating's partial rows (slice-strided, then the 32 slices in a fixed order);
+//    npr_r = p_r S_r; p_r <- npr_r / (eps + sum_r npr_r).
 //  blocks [p_blocks, ...): theta (:1016-1018), in place, one wave per gene:
 //      theta[g][a] <- theta[g][a] * (sum of the gene's contiguous c-scaled rows)[a] / deg[g]
-//    (rows in ascending CSR order per lane + fixed butterfly: reproducible).
+//    (fixed slot / accumulator / combine order: reproducible).
 // ------------------------------------------------------------------------------------------
-constexpr int MT_BATCH = 4;  // theta gather: rows in flight per lane
+constexpr int MP_CELLS = 8, MP_SLICES = 32;
 
 template <int K>
 __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double* __restrict__ theta,
                                                  const double* __restrict__ partS,
                                                  const double* __restrict__ contrib,
                                                  const int* __restrict__ gptr,
-                                                 const int* __restrict__ deg, int P, int R, int G,
-                                                 long long nnz, int p_blocks, double eps,
-                                                 int ablate) {
+                                                 const int* __restrict__ deg, SRows rg, int P,
+                                                 int R, int G, long long nnz, int p_blocks,
+                                                 double eps, int ablate) {
   constexpr int K3 = K * K * K;
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
@@ -887,52 +1229,71 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
   if ((int)blockIdx.x >= p_blocks) {  // --------------------------------------------- theta
     const int g = ((int)blockIdx.x - p_blocks) * 4 + (tid >> 6);
     if (g >= P || (ablate & 4)) return;  // wave-uniform
-    const double* __restrict__ cb = contrib + (size_t)b * nnz * K;
-    double acc[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    const double* __restrict__ cb = contrib + (size_t)b * (nnz + 1) * K;
+    // lane = (row slot, entry k): NS rows of K doubles per wave load (contiguous), four
+    // independent accumulators per lane, then the slots summed in a fixed order through LDS
+    constexpr int NS = 64 / K;
+    __shared__ double tred[4][64];
+    const int slot = lane / K, k = lane % K, wq = tid >> 6;
     const int q0 = gptr[g], q1 = gptr[g + 1];
-    for (int qb = q0; qb < q1; qb += 64 * MT_BATCH) {
-      double row[MT_BATCH][K];
-#pragma unroll
-      for (int j = 0; j < MT_BATCH; ++j) {
-        const int qq = qb + j * 64 + lane;
-        const double* __restrict__ src = cb + (size_t)(qq < q1 ? qq : q0) * K;
-#pragma unroll
-        for (int k = 0; k < K; ++k) row[j][k] = qq < q1 ? src[k] : 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (slot < NS) {
+      const double* __restrict__ src = cb + k;
+      int q = q0 + slot;
+      for (; q + 3 * NS < q1; q += 4 * NS) {
+        a0 += src[(size_t)q * K];
+        a1 += src[(size_t)(q + NS) * K];
+        a2 += src[(size_t)(q + 2 * NS) * K];
+        a3 += src[(size_t)(q + 3 * NS) * K];
       }
-#pragma unroll
-      for (int j = 0; j < MT_BATCH; ++j)
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc[k] += row[j][k];
+      for (; q < q1; q += NS) a0 += src[(size_t)q * K];
     }
-    double mine = 0.0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double t = wave_sum(acc[k]);
-      if (lane == k) mine = t;
-    }
+    tred[wq][lane] = (a0 + a1) + (a2 + a3);
+    wave_lds_sync();
     if (lane < K) {
+      double sum = 0.0;
+#pragma unroll
+      for (int q = 0; q < NS; ++q) sum += tred[wq][q * K + lane];
       double* row = theta + (size_t)b * P * K + (size_t)g * K;
-      row[lane] = row[lane] * mine / (double)deg[g];
+      row[lane] = row[lane] * sum / (double)deg[g];
     }
     return;
   }
-  const int cell = blockIdx.x * 4 + (tid >> 6);  // ------------------------------------- p
-  if (cell >= K3) return;  // wave-uniform
-  const double* __restrict__ rows = partS + (size_t)b * G * R * K3 + cell;
-  double npr[MAX_R];
-  double den = eps;
-  double* pc = pr + (size_t)b * R * K3 + cell;
+  // ------------------------------------------------------------------------------------ p
+  __shared__ double red[MAX_R][MP_SLICES][MP_CELLS];
+  const int cl = tid % MP_CELLS, sl = tid / MP_CELLS;
+  const int cell = blockIdx.x * MP_CELLS + cl;
+  const int cc = cell < K3 ? cell : K3 - 1;
+  const double* __restrict__ base = partS + (size_t)b * G * rg.rs * K3 + cc;
   for (int r = 0; r < R; ++r) {
-    double s = 0.0;
-    for (int w = lane; w < G; w += 64) s += rows[((size_t)w * R + r) * K3];
-    s = wave_sum(s);
-    npr[r] = pc[(size_t)r * K3] * s;
-    den += npr[r];
+    // four independent accumulators: the partial rows' loads overlap
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const size_t stride = (size_t)MP_SLICES * rg.rs * K3;
+    const double* __restrict__ src = base + ((size_t)(rg.wlo[r] + sl) * rg.rs + (size_t)r * rg.ro) * K3;
+    int w = rg.wlo[r] + sl;
+    for (; w + 3 * MP_SLICES < rg.whi[r]; w += 4 * MP_SLICES, src += 4 * stride) {
+      a0 += src[0];
+      a1 += src[stride];
+      a2 += src[2 * stride];
+      a3 += src[3 * stride];
+    }
+    for (; w < rg.whi[r]; w += MP_SLICES, src += stride) a0 += src[0];
+    red[r][sl][cl] = (a0 + a1) + (a2 + a3);
   }
-  if (lane == 0)
+  __syncthreads();
+  if (sl == 0 && cell < K3) {
+    double npr[MAX_R];
+    double den = eps;
+    double* pc = pr + (size_t)b * R * K3 + cell;
+    for (int r = 0; r < R; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < MP_SLICES; ++q) s += red[r][q][cl];
+      npr[r] = pc[(size_t)r * K3] * s;
+      den += npr[r];
+    }
     for (int r = 0; r < R; ++r) pc[(size_t)r * K3] = npr[r] / den;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1053,9 +1414,11 @@ struct LinkSet {
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Launch {
+  bool fused;  // emx_kernel compiled for this K
+  int (*emx)(mmsbm_ctx*, hipStream_t);
   int (*estep)(mmsbm_ctx*, hipStream_t);
   int (*m1)(mmsbm_ctx*, hipStream_t);
-  int (*m2)(mmsbm_ctx*, hipStream_t);
+  int (*m2)(mmsbm_ctx*, hipStream_t, bool);
   int (*loglik)(mmsbm_ctx*, int, const double*, const double*, hipStream_t);
   int (*predict)(mmsbm_ctx*, const int*, long long, const double*, const double*, double*,
                  hipStream_t);
@@ -1089,8 +1452,13 @@ struct mmsbm_ctx {
   int timing_stride = 1;  // time every n-th iteration
   int ablate = 0;  // MMSBM_ABLATE (measurement only)
   int sacc_wgs = SACC_WGS;  // S-accumulation workgroups requested (MMSBM_SACC_WGS)
-  int estep_variant = 0;    // 0: four lanes per observation where compiled; 1: two (MMSBM_ESTEP)
+  // MMSBM_ESTEP: 0 fused MFMA E-step + S where compiled (else 2); 1 two-lane VALU E-step + M1;
+  // 2 four-lane VALU E-step + M1
+  int estep_variant = 0;
   std::vector<hipEvent_t> ev[3];  // start/stop pairs per kernel id (E, M1, M2)
+  // MMSBM_TRACE (measurement only): per-wave phase cycles of the fused kernel's last launch
+  unsigned long long* trace = nullptr;
+  long long trace_waves = 0;
   size_t nev[3] = {0, 0, 0};
 };
 
@@ -1108,20 +1476,70 @@ int sacc_groups(const mmsbm_ctx* c) {
   return (int)(G > 0 ? G : 1);
 }
 
+// Workgroups of the fused kernel: each owns one rating; a rating gets a share of the requested
+// count proportional to its 16-observation groups (at least 1 when it has any, at most its
+// group count).  Returns the row description M2 reads and the total in *G.
+SRows fused_rows(const mmsbm_ctx* c, int* G) {
+  SRows rg{};
+  const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
+  const long long T = tr.n_obs_pad / XG;
+  const long long req = c->sacc_wgs < SACC_WGS_MAX ? c->sacc_wgs : SACC_WGS_MAX;
+  int w = 0;
+  rg.grp[0] = 0;
+  for (int r = 0; r < c->R; ++r) {
+    const long long lo = tr.seg.size() > (size_t)r ? tr.seg[r] / XG : 0;
+    const long long hi = tr.seg.size() > (size_t)r + 1 ? tr.seg[r + 1] / XG : 0;
+    const long long ng = hi - lo;
+    long long gr = 0;
+    if (ng > 0) {
+      gr = (long long)((double)req * (double)ng / (double)T + 0.5);
+      if (gr < 1) gr = 1;
+      if (gr > ng) gr = ng;
+    }
+    rg.grp[r + 1] = (int)hi;
+    rg.wlo[r] = w;
+    w += (int)gr;
+    rg.whi[r] = w;
+  }
+  rg.rs = 1;
+  rg.ro = 0;
+  *G = w > 0 ? w : 1;
+  return rg;
+}
+
+// M1 layout: every workgroup writes one row per rating.
+SRows m1_rows(const mmsbm_ctx* c) {
+  SRows rg{};
+  const int G = sacc_groups(c);
+  for (int r = 0; r < c->R; ++r) {
+    rg.wlo[r] = 0;
+    rg.whi[r] = G;
+  }
+  rg.rs = c->R;
+  rg.ro = 1;
+  return rg;
+}
+
 WsLayout ws_layout(const mmsbm_ctx* c) {
   WsLayout L{};
+  int GX = 1;
+  (void)fused_rows(c, &GX);
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
   const LinkSet& te = c->sets[MMSBM_SET_TEST];
   const size_t K3 = (size_t)c->K * c->K * c->K;
   size_t off = 0;
-  L.contrib = off;  // c-scaled (Y, Z, W) rows in gene-CSR order, 3 per observation
-  off += align_up((size_t)c->B * tr.n_obs_pad * 3 * c->K * sizeof(double));
+  // c-scaled (Y, Z, W) rows in gene-CSR order, 3 per observation, + one trash row per sample
+  // (row nnz: the fused kernel's stores for padding observations land there, branch-free)
+  L.contrib = off;
+  off += align_up((size_t)c->B * (tr.n_obs_pad * 3 + 1) * c->K * sizeof(double));
   L.cvec = off;
   off += align_up((size_t)c->B * tr.n_obs_pad * sizeof(double));
-  L.partS = off;  // [B][G][R][K3] partial S rows of the M1 workgroups
-  off += align_up((size_t)c->B * sacc_groups(c) * c->R * K3 * sizeof(double));
-  L.partL = off;  // one log-likelihood partial per 64-observation tile of either set
+  L.partS = off;  // partial S rows: [B][G][R][K3] (M1) or [B][GX][K3] (fused)
+  const size_t srows = std::max((size_t)sacc_groups(c) * c->R, (size_t)GX);
+  off += align_up((size_t)c->B * srows * K3 * sizeof(double));
+  L.partL = off;  // one log-likelihood partial per 64-observation tile / fused workgroup
   long long nt = (tr.n_obs_pad > te.n_obs_pad ? tr.n_obs_pad : te.n_obs_pad) / ET;
+  if (nt < GX) nt = GX;
   off += align_up((size_t)c->B * (nt > 0 ? nt : 1) * sizeof(double));
   L.total = off;
   return L;
@@ -1133,7 +1551,7 @@ int launch_estep(mmsbm_ctx* c, hipStream_t s) {
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
   if (tr.ntiles == 0) return MMSBM_OK;
   if constexpr (E4Plan<K>::ON) {
-    if (c->estep_variant == 0) {
+    if (c->estep_variant != 1) {
       const int nt = (int)(tr.n_obs_pad / ET);
       estep4_kernel<K><<<dim3(nt, c->B), E4_NT, E4Plan<K>::LDS_BYTES, s>>>(
           tr.obs, reinterpret_cast<const int4*>(c->pos), tr.tile_r, c->theta_mut, c->pr_mut,
@@ -1169,14 +1587,44 @@ int launch_m1(mmsbm_ctx* c, hipStream_t s) {
 }
 
 template <int K>
-int launch_m2(mmsbm_ctx* c, hipStream_t s) {
+int launch_emx(mmsbm_ctx* c, hipStream_t s) {
+  if constexpr (XPlan<K>::ON) {
+    const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
+    if (tr.ntiles == 0) return MMSBM_OK;
+    int G = 1;
+    const SRows rg = fused_rows(c, &G);
+    static bool attr = false;  // LDS above 64 KB needs the opt-in once per kernel
+    if (!attr) {
+      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&emx_kernel<K>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, XPlan<K>::LDS_BYTES));
+      attr = true;
+    }
+    emx_kernel<K><<<dim3(G, c->B), XPlan<K>::NT, XPlan<K>::LDS_BYTES, s>>>(
+        tr.obs, reinterpret_cast<const int4*>(c->pos), c->theta_mut, c->pr_mut, c->contrib,
+        c->partS, c->partL, rg, c->P, c->R, c->nnz, G, c->eps, XTrace{c->trace});
+    c->trace_waves = (long long)G * c->B * XPlan<K>::NW;
+    HIP_TRY(hipGetLastError());
+    return MMSBM_OK;
+  } else {
+    return fail(MMSBM_ERR_UNSUPPORTED, "fused E-step not compiled for K=%d", K);
+  }
+}
+
+template <int K>
+int launch_m2(mmsbm_ctx* c, hipStream_t s, bool fused) {
   constexpr int K3 = K * K * K;
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
   if (tr.ntiles == 0) return MMSBM_OK;
-  const int p_blocks = (K3 + 3) / 4;
+  int G = sacc_groups(c);
+  SRows rg;
+  if (fused)
+    rg = fused_rows(c, &G);
+  else
+    rg = m1_rows(c);
+  const int p_blocks = (K3 + MP_CELLS - 1) / MP_CELLS;
   const int theta_blocks = (c->P + 3) / 4;
   m2_kernel<K><<<dim3(p_blocks + theta_blocks, c->B), 256, 0, s>>>(
-      c->pr_mut, c->theta_mut, c->partS, c->contrib, c->gptr, c->deg, c->P, c->R, sacc_groups(c),
+      c->pr_mut, c->theta_mut, c->partS, c->contrib, c->gptr, c->deg, rg, c->P, c->R, G,
       c->nnz, p_blocks, c->eps, c->ablate);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
@@ -1206,8 +1654,8 @@ int launch_predict(mmsbm_ctx* c, const int* ids, long long n, const double* thet
 template <int... Ks>
 constexpr auto make_table(std::integer_sequence<int, Ks...>) {
   return std::array<Launch, sizeof...(Ks)>{
-      Launch{&launch_estep<Ks + 1>, &launch_m1<Ks + 1>, &launch_m2<Ks + 1>, &launch_loglik<Ks + 1>,
-             &launch_predict<Ks + 1>}...};
+      Launch{XPlan<Ks + 1>::ON, &launch_emx<Ks + 1>, &launch_estep<Ks + 1>, &launch_m1<Ks + 1>,
+             &launch_m2<Ks + 1>, &launch_loglik<Ks + 1>, &launch_predict<Ks + 1>}...};
 }
 
 const auto kTable = make_table(std::make_integer_sequence<int, MMSBM_MAX_K>{});
@@ -1250,6 +1698,10 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   c->device = device;
   if (const char* ab = getenv("MMSBM_ABLATE")) c->ablate = atoi(ab);
   if (const char* v = getenv("MMSBM_ESTEP")) c->estep_variant = atoi(v);
+  if (getenv("MMSBM_TRACE")) {
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipMalloc(&c->trace, sizeof(unsigned long long) * 16 * 65536));
+  }
   if (const char* t = getenv("MMSBM_SACC_WGS")) {
     const int v = atoi(t);
     if (v >= 1) c->sacc_wgs = v;
@@ -1264,6 +1716,7 @@ int mmsbm_destroy(mmsbm_ctx* c) {
   for (auto& s : c->sets)
     if (s.tile_r) (void)hipFree(s.tile_r);
   if (c->pos) (void)hipFree(c->pos);
+  if (c->trace) (void)hipFree(c->trace);
   for (auto& v : c->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   delete c;
@@ -1405,17 +1858,37 @@ int mmsbm_iterate(mmsbm_ctx* c, double* theta, double* pr, int32_t n_iters, void
   const Launch& L = kTable[c->K - 1];
   c->theta_mut = theta;
   c->pr_mut = pr;
+  const bool fused = L.fused && c->estep_variant == 0;
   for (int it = 0; it < n_iters; ++it) {
     const bool mark = c->timing && (it % c->timing_stride == 0);
     if (mark && (rc = timing_mark(c, 0, s))) return rc;
-    if ((rc = L.estep(c, s))) return rc;
+    if ((rc = fused ? L.emx(c, s) : L.estep(c, s))) return rc;
     if (mark && (rc = timing_mark(c, 0, s))) return rc;
-    if (mark && (rc = timing_mark(c, 1, s))) return rc;
-    if ((rc = L.m1(c, s))) return rc;
-    if (mark && (rc = timing_mark(c, 1, s))) return rc;
+    if (!fused) {
+      if (mark && (rc = timing_mark(c, 1, s))) return rc;
+      if ((rc = L.m1(c, s))) return rc;
+      if (mark && (rc = timing_mark(c, 1, s))) return rc;
+    }
     if (mark && (rc = timing_mark(c, 2, s))) return rc;
-    if ((rc = L.m2(c, s))) return rc;
+    if ((rc = L.m2(c, s, fused))) return rc;
     if (mark && (rc = timing_mark(c, 2, s))) return rc;
+  }
+  if (c->trace && fused && n_iters > 0) {  // measurement only: phase cycles of the last launch
+    const long long nw = c->trace_waves < 65536 ? c->trace_waves : 65536;
+    std::vector<unsigned long long> h(nw * 16);
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemcpy(h.data(), c->trace, h.size() * 8, hipMemcpyDeviceToHost));
+    double sum[9] = {0};
+    unsigned long long mx = 0;
+    for (long long i = 0; i < nw; ++i) {
+      for (int q = 0; q < 9; ++q) sum[q] += (double)h[i * 16 + q];
+      mx = std::max(mx, h[i * 16 + 8]);
+    }
+    fprintf(stderr,
+            "[mmsbm trace] waves=%lld avg cycles: prologue %.0f  U %.0f  KR %.0f  W %.0f  "
+            "stores %.0f  S %.0f  epilogue %.0f  groups %.2f  total %.0f (max %llu)\n",
+            nw, sum[0] / nw, sum[1] / nw, sum[2] / nw, sum[3] / nw, sum[4] / nw, sum[5] / nw,
+            sum[6] / nw, sum[7] / nw, sum[8] / nw, mx);
   }
   return MMSBM_OK;
 }
