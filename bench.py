@@ -31,7 +31,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector: 256 CU x 128 FLOP/clk x 2.4 GHz (spec)
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector and matrix: 256 CU x 128 FLOP/clk x 2.4 GHz (spec)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -170,9 +170,12 @@ def main():
     if rank == 0:
         iters_total = args.steps * B * world
         value = iters_total / elapsed
-        # roofline of the dominant kernel (E-step), per launch; SURVEY.md §8d figures
+        # roofline of the dominant kernel (the E-step), per launch; SURVEY.md §8d figures.
+        # Fused path (FP64 MFMA): the E-step launch does Y, Z, W and S = 8 K^3 per observation;
+        # VALU path: the E-step does Y, Z, W = 6 K^3 (S is M1's 2 K^3).
+        fused = eng.fused
         est_avg_s = est_ms / 1e3 / est_n if est_n else float("nan")
-        flops = 8.0 * K ** 3 * E_obs * B
+        flops = (8.0 if fused else 6.0) * K ** 3 * E_obs * B
         hbm_bytes = (16.0 * E_obs + 16.0 * host.P * K + 24.0 * K ** 3 * 2) * B
         achieved_tf = flops / est_avg_s / 1e12
         traffic = None
@@ -180,7 +183,7 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 rec = json.load(f)
-            if rec.get("E_obs") == E_obs and rec.get("B") == B:
+            if rec.get("E_obs") == E_obs and rec.get("B") == B and rec.get("fused") == fused:
                 traffic = rec.get("hbm_bytes_per_launch")
         line = {
             "metric": "EM-iterations/sec + final log-likelihood, fold0 K=%d" % K,
@@ -200,9 +203,12 @@ def main():
                        "E_obs": E_obs, "samples_per_gpu": B, "parallelism": "restart-sharded x%d" % world},
             "final_loglik": float(L_all[0]),
             "final_loglik_best": float(L_all.max()),
-            "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": "estep_kernel<%d>" % K, "avg_launch_us": est_avg_s * 1e6,
+            "roofline": {"bound": "mfma" if fused else "fp64-valu", "achieved": achieved_tf,
+                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "kernel": ("emx_kernel<%d> (E-step + S, FP64 MFMA)" if fused
+                                    else "estep_kernel<%d> (VALU)") % K,
+                         "avg_launch_us": est_avg_s * 1e6,
                          "algorithmic_flops_per_launch": flops,
                          "hbm": {"achieved": hbm_bytes / est_avg_s / 1e9, "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": hbm_bytes / est_avg_s / 1e9 / HBM_PEAK_GBS,

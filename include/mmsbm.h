@@ -103,6 +103,11 @@ int mmsbm_loglik(mmsbm_ctx *ctx, int32_t which, const double *theta, const doubl
 int mmsbm_predict(mmsbm_ctx *ctx, const int32_t *ids, int64_t n, const double *theta,
                   const double *pr, double *out, void *stream);
 
+/* *fused = 1 when mmsbm_iterate runs the fused FP64-MFMA E-step (E-step and S accumulation in
+ * one kernel, then M2), 0 when it runs the VALU E-step + M1 + M2 (MMSBM_ESTEP, or K outside the
+ * fused kernel's range). */
+int mmsbm_fused(const mmsbm_ctx *ctx, int32_t *fused);
+
 /* Kernel timing for measurement (bench.py): with stride n > 0, mmsbm_iterate records a HIP
  * event pair on the launch stream around every kernel of every n-th iteration (kernel ids:
  * 0 E-step, 1 M1 = S accumulation + theta gather, 2 M2 = p update); 0 disables.

@@ -910,7 +910,8 @@ struct XPlan {
   static constexpr int KRS = KRW + 2;         // row stride = 2 (mod 4): conflict-free W reads
   static constexpr int NT4 = (K2 + 15) / 16;  // S-phase 16-cell tiles
   static constexpr int SACC = NT4 * NG;       // S accumulators per lane
-  static constexpr int P_DBL = K * KP * KP;   // p_r image [a][b][g], b and g zero padded
+  static constexpr int PW_ROWS = K2 + KP;     // p_r image rows (a, b) = a K + b, zero padded
+  static constexpr int P_DBL = PW_ROWS * KP;  // p_r image [(a, b)][g], g zero padded
   static constexpr int IMG = 3 * XG * KP;     // th_i / th_j / th_k rows of the wave's group
   static constexpr int WAVE_DBL = XG * KRS + IMG;
   static constexpr int NW = (P_DBL + 8 * WAVE_DBL + 8) * 8 <= 160 * 1024 ? 8 : 4;
@@ -958,7 +959,7 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
   constexpr int NG = X::NG, KP = X::KP, K2 = X::K2, K3 = X::K3, NC = X::NC, NT4 = X::NT4;
   constexpr int KRS = X::KRS, KRW = X::KRW, NW = X::NW, NT = X::NT, SACC = X::SACC;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* Pl = smem;  // [K][KP][KP]
+  double* Pw = smem;  // [K^2 + KP][KP] p_r, row a K + b, columns g
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* KR = smem + X::P_DBL + wv * X::WAVE_DBL;  // [XG][KRS]
@@ -1004,8 +1005,8 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
   }
 
   for (int idx = tid; idx < X::P_DBL; idx += NT) {
-    const int g = idx % KP, bq = (idx / KP) % KP, a = idx / (KP * KP);
-    Pl[idx] = (g < K && bq < K) ? p[(a * K + bq) * K + g] : 0.0;
+    const int g = idx % KP, row = idx / KP;
+    Pw[idx] = (g < K && row < K2) ? p[row * K + g] : 0.0;
   }
   if constexpr (KRW > K2) {  // pad cells of the W-phase k-steps stay 0
     for (int idx = lane; idx < XG * (KRW - K2); idx += 64)
@@ -1051,7 +1052,8 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
 #pragma unroll
       for (int bb = 0; bb < NG; ++bb)
 #pragma unroll
-        for (int s = 0; s < NG; ++s) bf[bb][s] = Pl[(a * KP + 4 * bb + lo) * KP + 4 * s + hi];
+        for (int s = 0; s < NG; ++s)  // b = 4 bb + lo >= K reads the next row: finite, and
+          bf[bb][s] = Pw[(a * K + 4 * bb + lo) * KP + 4 * s + hi];  // th_j[b] = 0 drops it
       double acc[NG];
 #pragma unroll
       for (int bb = 0; bb < NG; ++bb) acc[bb] = 0.0;
@@ -1112,9 +1114,8 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
 #pragma unroll
     for (int s = 0; s < NC; ++s) {
       const int cell = 4 * s + hi;
-      const int cc = cell < K2 ? cell : K2 - 1;
       const double av = KRo[cell];
-      const double* pb = Pl + ((cc / K) * KP + cc % K) * KP + lo;
+      const double* pb = Pw + cell * KP + lo;  // rows >= K^2 are zero (KR is zero there too)
 #pragma unroll
       for (int u = 0; u < NG; ++u) wacc[u] = mfma4(av, pb[4 * u], wacc[u]);
     }
@@ -1204,15 +1205,18 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// M2, grid (p_blocks + theta_blocks, B), block 256.
-//  blocks [0, p_blocks): p (:1021-1028), 8 cells x 32 row slices per block: S_r = sum of the
-//    rating's partial rows (slice-strided, then the 32 slices in a fixed order);
-//    npr_r = p_r S_r; p_r <- npr_r / (eps + sum_r npr_r).
-//  blocks [p_blocks, ...): theta (:1016-1018), in place, one wave per gene:
+// M2, grid (p_blocks + P, B), block 256.
+//  blocks [0, p_blocks): p (:1021-1028), 8 cells x 32 row slices per block.  Partial row n
+//    (n < NR = G * rs) sits at partS + (b * NR + n) * K3 and belongs to rating n % R (M1
+//    layout) or to the rating whose workgroup range holds n (fused layout).  Each thread loads
+//    its rows MP_UNROLL at a time (one memory round trip for up to 256 rows), keeps a sum per
+//    rating, then the 32 slices are added in a fixed order; npr_r = p_r S_r;
+//    p_r <- npr_r / (eps + sum_r npr_r).
+//  blocks [p_blocks, ...): theta (:1016-1018), in place, one workgroup per gene:
 //      theta[g][a] <- theta[g][a] * (sum of the gene's contiguous c-scaled rows)[a] / deg[g]
-//    (fixed slot / accumulator / combine order: reproducible).
+//    thread = (row slot, entry a); fixed slot / accumulator / combine order: reproducible.
 // ------------------------------------------------------------------------------------------
-constexpr int MP_CELLS = 8, MP_SLICES = 32;
+constexpr int MP_CELLS = 8, MP_SLICES = 32, MP_UNROLL = 8;
 
 template <int K>
 __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double* __restrict__ theta,
@@ -1225,20 +1229,16 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
   constexpr int K3 = K * K * K;
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
   if ((int)blockIdx.x >= p_blocks) {  // --------------------------------------------- theta
-    const int g = ((int)blockIdx.x - p_blocks) * 4 + (tid >> 6);
-    if (g >= P || (ablate & 4)) return;  // wave-uniform
-    const double* __restrict__ cb = contrib + (size_t)b * (nnz + 1) * K;
-    // lane = (row slot, entry k): NS rows of K doubles per wave load (contiguous), four
-    // independent accumulators per lane, then the slots summed in a fixed order through LDS
-    constexpr int NS = 64 / K;
-    __shared__ double tred[4][64];
-    const int slot = lane / K, k = lane % K, wq = tid >> 6;
+    const int g = (int)blockIdx.x - p_blocks;
+    if (g >= P || (ablate & 4)) return;  // workgroup-uniform
+    constexpr int NS = 256 / K;          // row slots
+    __shared__ double tred[256];
+    const int slot = tid / K, k = tid % K;
     const int q0 = gptr[g], q1 = gptr[g + 1];
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     if (slot < NS) {
-      const double* __restrict__ src = cb + k;
+      const double* __restrict__ src = contrib + (size_t)b * (nnz + 1) * K + k;
       int q = q0 + slot;
       for (; q + 3 * NS < q1; q += 4 * NS) {
         a0 += src[(size_t)q * K];
@@ -1248,14 +1248,14 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
       }
       for (; q < q1; q += NS) a0 += src[(size_t)q * K];
     }
-    tred[wq][lane] = (a0 + a1) + (a2 + a3);
-    wave_lds_sync();
-    if (lane < K) {
+    tred[tid] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (tid < K) {
       double sum = 0.0;
 #pragma unroll
-      for (int q = 0; q < NS; ++q) sum += tred[wq][q * K + lane];
+      for (int q = 0; q < NS; ++q) sum += tred[q * K + tid];
       double* row = theta + (size_t)b * P * K + (size_t)g * K;
-      row[lane] = row[lane] * sum / (double)deg[g];
+      row[tid] = row[tid] * sum / (double)deg[g];
     }
     return;
   }
@@ -1264,35 +1264,52 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
   const int cl = tid % MP_CELLS, sl = tid / MP_CELLS;
   const int cell = blockIdx.x * MP_CELLS + cl;
   const int cc = cell < K3 ? cell : K3 - 1;
-  const double* __restrict__ base = partS + (size_t)b * G * rg.rs * K3 + cc;
-  for (int r = 0; r < R; ++r) {
-    // four independent accumulators: the partial rows' loads overlap
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    const size_t stride = (size_t)MP_SLICES * rg.rs * K3;
-    const double* __restrict__ src = base + ((size_t)(rg.wlo[r] + sl) * rg.rs + (size_t)r * rg.ro) * K3;
-    int w = rg.wlo[r] + sl;
-    for (; w + 3 * MP_SLICES < rg.whi[r]; w += 4 * MP_SLICES, src += 4 * stride) {
-      a0 += src[0];
-      a1 += src[stride];
-      a2 += src[2 * stride];
-      a3 += src[3 * stride];
+  const int NR = G * rg.rs;
+  const double* __restrict__ base = partS + (size_t)b * NR * K3 + cc;
+  double acc[MAX_R];
+#pragma unroll
+  for (int q = 0; q < MAX_R; ++q) acc[q] = 0.0;
+  for (int n0 = 0; n0 < NR; n0 += MP_SLICES * MP_UNROLL) {
+    double v[MP_UNROLL];
+#pragma unroll
+    for (int j = 0; j < MP_UNROLL; ++j) {
+      const int n = n0 + sl + j * MP_SLICES;
+      v[j] = n < NR ? base[(size_t)n * K3] : 0.0;
     }
-    for (; w < rg.whi[r]; w += MP_SLICES, src += stride) a0 += src[0];
-    red[r][sl][cl] = (a0 + a1) + (a2 + a3);
+#pragma unroll
+    for (int j = 0; j < MP_UNROLL; ++j) {
+      const int n = n0 + sl + j * MP_SLICES;
+      if (n < NR) {
+        int rr = 0;
+        if (rg.rs == 1) {
+#pragma unroll
+          for (int q = 1; q < MAX_R; ++q)
+            if (q < R && n >= rg.wlo[q]) rr = q;
+        } else {
+          rr = n % R;
+        }
+#pragma unroll
+        for (int q = 0; q < MAX_R; ++q)
+          if (q == rr) acc[q] += v[j];
+      }
+    }
   }
+#pragma unroll
+  for (int q = 0; q < MAX_R; ++q)
+    if (q < R) red[q][sl][cl] = acc[q];
   __syncthreads();
   if (sl == 0 && cell < K3) {
     double npr[MAX_R];
     double den = eps;
     double* pc = pr + (size_t)b * R * K3 + cell;
-    for (int r = 0; r < R; ++r) {
+    for (int q = 0; q < R; ++q) {
       double s = 0.0;
 #pragma unroll
-      for (int q = 0; q < MP_SLICES; ++q) s += red[r][q][cl];
-      npr[r] = pc[(size_t)r * K3] * s;
-      den += npr[r];
+      for (int z = 0; z < MP_SLICES; ++z) s += red[q][z][cl];
+      npr[q] = pc[(size_t)q * K3] * s;
+      den += npr[q];
     }
-    for (int r = 0; r < R; ++r) pc[(size_t)r * K3] = npr[r] / den;
+    for (int q = 0; q < R; ++q) pc[(size_t)q * K3] = npr[q] / den;
   }
 }
 
@@ -1622,7 +1639,7 @@ int launch_m2(mmsbm_ctx* c, hipStream_t s, bool fused) {
   else
     rg = m1_rows(c);
   const int p_blocks = (K3 + MP_CELLS - 1) / MP_CELLS;
-  const int theta_blocks = (c->P + 3) / 4;
+  const int theta_blocks = c->P;  // one workgroup per gene
   m2_kernel<K><<<dim3(p_blocks + theta_blocks, c->B), 256, 0, s>>>(
       c->pr_mut, c->theta_mut, c->partS, c->contrib, c->gptr, c->deg, rg, c->P, c->R, G,
       c->nnz, p_blocks, c->eps, c->ablate);
@@ -1924,6 +1941,14 @@ int mmsbm_predict(mmsbm_ctx* c, const int32_t* ids, int64_t n, const double* the
     return fail(MMSBM_ERR_INVALID, "bad arguments");
   HIP_TRY(hipSetDevice(c->device));
   return kTable[c->K - 1].predict(c, ids, n, theta, pr, out, (hipStream_t)stream);
+}
+
+int mmsbm_fused(const mmsbm_ctx* c, int32_t* fused) {
+  if (!c || !fused) return fail(MMSBM_ERR_INVALID, "null argument");
+  int rc = check_shape(c);
+  if (rc) return rc;
+  *fused = kTable[c->K - 1].fused && c->estep_variant == 0 ? 1 : 0;
+  return MMSBM_OK;
 }
 
 int mmsbm_timing(mmsbm_ctx* c, int32_t stride) {

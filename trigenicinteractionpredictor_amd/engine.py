@@ -124,6 +124,13 @@ class EMEngine:
     # ---------------------------------------------------------- measurement
     KERNELS = ("estep", "m1", "m2")
 
+    @property
+    def fused(self) -> bool:
+        """True when iterate() runs the fused FP64-MFMA E-step (E-step + S in one kernel)."""
+        v = ctypes.c_int32()
+        _lib.check(self.lib.mmsbm_fused(self.ctx, ctypes.byref(v)))
+        return bool(v.value)
+
     def timing(self, stride: int = 1):
         """Record HIP event pairs around the kernels of every `stride`-th iteration (0: off)."""
         _lib.check(self.lib.mmsbm_timing(self.ctx, int(stride)))
