@@ -114,6 +114,13 @@ int mmsbm_fused(const mmsbm_ctx *ctx, int32_t *fused);
  * mmsbm_timing resets the counters; mmsbm_timing_result waits for the last event and returns
  * the summed device time (ms) and the number of timed launches of that kernel. */
 int mmsbm_timing(mmsbm_ctx *ctx, int32_t stride);
+
+/* Measurement: n back-to-back launches of the E-step kernel mmsbm_iterate would run (the fused
+ * kernel, or the VALU E-step) on the current theta / pr, between one HIP event pair on
+ * `stream`; *avg_ms = elapsed / n.  The E-step only reads theta / pr, so the parameters are
+ * unchanged.  Synchronises the stream. */
+int mmsbm_time_estep(mmsbm_ctx *ctx, double *theta, double *pr, int32_t n, void *stream,
+                     double *avg_ms);
 int mmsbm_timing_result(mmsbm_ctx *ctx, int32_t kernel, double *total_ms, int64_t *count);
 
 #ifdef __cplusplus

@@ -1,0 +1,108 @@
+"""The CLI driver (reference `__main__`, src/TrigenicInteractionPredictor.py:1148-1279): flag
+parsing and validation, the check schedule, convergence, output naming and the skip-if-exists
+resume rule — on CPU, with the oracle standing in for the GPU model."""
+import contextlib
+import io
+import math
+import os
+import random
+
+import pytest
+
+from oracle.mmsbm_oracle import OracleModel
+from trigenicinteractionpredictor_amd import cli
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tiny")
+TRAIN, TEST = os.path.join(GOLD, "train.dat"), os.path.join(GOLD, "test.dat")
+
+
+class OracleCliModel(OracleModel):
+    """Oracle model with the drop-in's batch call and a minimal to_file (test stand-in)."""
+    written = []
+
+    def make_iterations(self, n):
+        for _ in range(n):
+            self.make_iteration()
+
+    def to_file(self, name):
+        with open(name, "w") as f:
+            f.write("Max Likelihood:\t%r\n" % self.compute_likelihood())
+        OracleCliModel.written.append(name)
+
+
+def _reference_loop(K, seed, samples, iterations, f, b):
+    """The reference __main__ per-sample loop (:1253-1279) on the oracle, one make_iteration at a
+    time: (sample, iterations run, converged, final likelihood)."""
+    m = OracleModel()
+    with contextlib.redirect_stdout(io.StringIO()):
+        m.get_traintest(TRAIN, TEST)
+    random.seed(seed)
+    out = []
+    for s in range(samples):
+        m.initialize_parameters(K)
+        like0 = m.compute_likelihood()
+        done = None
+        for it in range(iterations):
+            m.make_iteration()
+            if it % f == 0 and it > b:
+                like = m.compute_likelihood()
+                if math.fabs((like - like0) / like0) < 0.01:
+                    done = (s, it + 1, True)
+                    break
+                like0 = like
+        out.append(done or (s, iterations, False))
+    return out
+
+
+def _run(argv):
+    lines = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        rc = cli.main(argv, model_factory=OracleCliModel, out=lines.append)
+    return rc, lines
+
+
+def test_check_points_follow_the_reference_condition():
+    assert cli.check_points(10, 3, 4) == [6, 9]
+    assert cli.check_points(200, 25, 100) == [125, 150, 175]
+    assert cli.check_points(50, 51, 0) == []      # -f 0 with -i 50: never checks
+
+
+def test_driver_matches_reference_loop(tmp_path):
+    OracleCliModel.written = []
+    out = str(tmp_path) + os.sep
+    rc, lines = _run(["-k", "2", "-i", "40", "-n", "3", "-f", "3", "-b", "4", "-t", TRAIN,
+                      "-e", TEST, "-o", out, "--seed", "5"])
+    assert rc == 0
+    ref = _reference_loop(2, 5, 3, 40, 3, 4)
+    iters = [l for l in lines if l.startswith("· Iteration ")]
+    assert len(iters) == sum(r[1] for r in ref)
+    conv = [r for r in ref if r[2]]
+    assert sorted(OracleCliModel.written) == sorted(out + "Sample_%d_K2.csv" % r[0] for r in conv)
+    # resume: finished samples are skipped on a second run
+    OracleCliModel.written = []
+    rc, lines = _run(["-k", "2", "-i", "40", "-n", "3", "-f", "3", "-b", "4", "-t", TRAIN,
+                      "-e", TEST, "-o", out, "--seed", "5"])
+    assert rc == 0
+    assert sum(1 for l in lines if l.startswith("Sample ")) == 3 - len(conv)
+
+
+def test_fcheck_zero_never_writes(tmp_path):
+    OracleCliModel.written = []
+    rc, lines = _run(["-i", "8", "-f", "0", "-k", "2", "-n", "1", "-t", TRAIN, "-e", TEST,
+                      "-o", str(tmp_path) + os.sep, "--seed", "1"])
+    assert rc == 0 and OracleCliModel.written == []
+    assert sum(1 for l in lines if l.startswith("· Iteration ")) == 8
+    assert not any(l.startswith("· Likelihood ") for l in lines)
+
+
+@pytest.mark.parametrize("argv", [["-i", "0"], ["-n", "0"], ["-s", "-1"], ["-f", "-1"], ["-b", "-2"],
+                                  ["-k", "0"], ["-t", "/nonexistent.dat"], ["-o", "/nonexistent/"],
+                                  ["-x"], ["-i", "abc"]])
+def test_invalid_arguments_exit_2(argv):
+    rc, _ = _run(argv)
+    assert rc == 2
+
+
+def test_help_exits_0():
+    rc, _ = _run(["-h"])
+    assert rc == 0

@@ -1,0 +1,34 @@
+"""The CLI driver on the GPU model: same iterations-to-convergence and output files as the
+reference loop run on the oracle (src/TrigenicInteractionPredictor.py:1253-1279), and the
+output header of `to_string` (:847-858) with the likelihoods within the parity tolerance."""
+import contextlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+from test_cli import TEST, TRAIN, _reference_loop
+from trigenicinteractionpredictor_amd import cli
+
+pytestmark = pytest.mark.gpu
+
+
+def test_cli_on_gpu_matches_reference_loop(tmp_path):
+    out = str(tmp_path) + os.sep
+    lines = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        rc = cli.main(["-k", "3", "-i", "60", "-n", "2", "-f", "4", "-b", "6", "-t", TRAIN, "-e", TEST,
+                       "-o", out, "--seed", "7"], out=lines.append)
+    assert rc == 0
+    ref = _reference_loop(3, 7, 2, 60, 4, 6)
+    assert sum(1 for l in lines if l.startswith("· Iteration ")) == sum(r[1] for r in ref)
+    for s, _, conv in ref:
+        path = out + "Sample_%d_K3.csv" % s
+        assert os.path.isfile(path) == conv
+        if conv:
+            text = open(path).read()
+            assert text.startswith("Max Likelihood:\t")
+            assert "Held-out Likelihood:\t" in text and "\nMetrics:\n" in text
+            like = float(text.split("\n")[0].split("\t")[1])
+            assert np.isfinite(like)

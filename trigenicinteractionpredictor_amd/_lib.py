@@ -41,6 +41,7 @@ SIGNATURES = {
     "mmsbm_predict": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _vp, _vp]),
     "mmsbm_fused": (_c_int, [_vp, ctypes.POINTER(_c_i32)]),
     "mmsbm_timing": (_c_int, [_vp, _c_i32]),
+    "mmsbm_time_estep": (_c_int, [_vp, _vp, _vp, _c_i32, _vp, ctypes.POINTER(_c_dbl)]),
     "mmsbm_timing_result": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_i64)]),
 }
 

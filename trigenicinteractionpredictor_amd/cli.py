@@ -1,0 +1,186 @@
+"""Command-line driver: the reference's `__main__` (src/TrigenicInteractionPredictor.py:1148-1279)
+on the GPU `Model`.
+
+    python -m trigenicinteractionpredictor_amd.cli -k 10 -t train0.dat -e test0.dat -o out/ \
+        [-i 10000] [-n 100] [-s 0] [-f 25] [-b 100] [--seed S]
+
+Same flags, defaults, validation, exit codes and per-sample semantics as the reference:
+  * `random.seed(os.getpid())` once (:1149) unless --seed is given (an addition, for
+    reproducible runs); samples consume the stdlib stream one after another;
+  * a sample whose `Sample_<n>_K<k>.csv` exists is skipped (:1256-1257, the resume rule);
+  * the likelihood is checked after iteration `it` when `it % f == 0 and it > b` (:1268) and
+    the sample stops when |(L - L0) / L0| < 0.01 (:1272), writing its file only then (:1275);
+  * `-f 0` sets f = iterations + 1 with the iterations value parsed so far (:1192-1193), so
+    the check never fires and no file is written — kept, not "fixed";
+  * the K = 1 warning never prints (`int(arg == 1)`, :1224) — kept.
+The iterations between two checks run as one `Model.make_iterations(n)` call (no host round
+trip per iteration); the per-iteration lines are printed after the batch, with the same text.
+"""
+from __future__ import annotations
+
+import getopt
+import math
+import os
+import random
+import sys
+
+USAGE = """
+Usage:
+python -m trigenicinteractionpredictor_amd.cli [-h|--help] [-i|--num_iterations=] <iterations>
+    [-n|--num_samples=] <samples> [-s|--sample_ini=] <first sample id>
+    [-f|--fcheck=] <likelihood check frequency, 0: never> [-b|--bcheck=] <first check after>
+    [-o|--out=] <output path prefix> [-t|--train=] <train file> [-e|--test=] <test file>
+    [-k|--k=] <number of groups> [--seed=] <RNG seed, default: the process id>
+
+Defaults: iterations {it}, samples {s}, check frequency {f}, train file {t}, K {k}.
+"""
+
+
+class ArgError(Exception):
+    pass
+
+
+def parse(argv, defaults):
+    cfg = dict(defaults)
+    try:
+        opts, _ = getopt.getopt(argv, "hi:n:s:f:b:o:t:e:k:",
+                                ["help", "num_iterations=", "num_samples=", "sample_ini=", "fcheck=",
+                                 "bcheck=", "out=", "train=", "test=", "k=", "seed="])
+    except getopt.GetoptError:
+        print("Argument error. Aborting")
+        raise ArgError()
+    for opt, arg in opts:          # in order: -f 0 uses the iterations parsed before it
+        if opt in ("-h", "--help"):
+            print(USAGE.format(it=cfg["iterations"], s=cfg["samples"], f=cfg["fcheck"],
+                               t=cfg["train"], k=cfg["k"]))
+            cfg["help"] = True
+            return cfg
+        try:
+            if opt in ("-i", "--num_iterations"):
+                if int(arg) < 1:
+                    print("\n\nERROR: Number of num_iterations should be a integer positive number!")
+                    raise ArgError()
+                cfg["iterations"] = int(arg)
+            elif opt in ("-n", "--num_samples"):
+                if int(arg) < 1:
+                    print("\n\nERROR: Number of samples should be a integer positive number")
+                    raise ArgError()
+                cfg["samples"] = int(arg)
+            elif opt in ("-s", "--sample_ini"):
+                if int(arg) < 0:
+                    print("\n\nERROR: Number of samples should be a integer positive number!")
+                    raise ArgError()
+                cfg["sample_ini"] = int(arg)
+            elif opt in ("-f", "--fcheck"):
+                if int(arg) < 0:
+                    print("\n\nERROR: frequency of checking should be a integer positive number or 0!")
+                    raise ArgError()
+                cfg["fcheck"] = cfg["iterations"] + 1 if int(arg) == 0 else int(arg)
+            elif opt in ("-b", "--bcheck"):
+                if int(arg) < 0:
+                    print("\n\nERROR: Threshold to start checking likelihood should be a integer "
+                          "positive number or 0!")
+                    raise ArgError()
+                cfg["bcheck"] = int(arg)
+            elif opt in ("-o", "--out"):
+                if not os.path.exists(str(arg)):
+                    print("\n\nERROR: The selected path does not exist.")
+                    raise ArgError()
+                cfg["out"] = arg
+            elif opt in ("-t", "--train"):
+                if not os.path.isfile(arg):
+                    print("\n\nERROR: The selected file does not exist.")
+                    raise ArgError()
+                cfg["train"] = arg
+            elif opt in ("-e", "--test"):
+                if not os.path.isfile(arg):
+                    print("\n\nERROR: The selected file does not exist.")
+                    raise ArgError()
+                cfg["test"] = arg
+            elif opt in ("-k", "--k"):
+                if int(arg) < 1:
+                    print("\n\nERROR: Number of groups should be a positive integer number different from 0")
+                    raise ArgError()
+                cfg["k"] = int(arg)
+            elif opt == "--seed":
+                cfg["seed"] = int(arg)
+        except ValueError:
+            raise ArgError()
+    return cfg
+
+
+def check_points(iterations, fcheck, bcheck):
+    """Iteration indices after which the reference checks the likelihood (:1268)."""
+    return [it for it in range(iterations) if it % fcheck == 0 and it > bcheck]
+
+
+def run_sample(model, cfg, sample, outfile, out=print):
+    """One sample of the reference loop (:1259-1279); returns (iterations run, converged)."""
+    out("Sample " + str(sample) + ":")
+    model.initialize_parameters(cfg["k"])
+    out("Parameters have been initialized")
+    like0 = model.compute_likelihood()
+    out("· Initial Likelihood is " + str(like0))
+    iterations, f, b = cfg["iterations"], cfg["fcheck"], cfg["bcheck"]
+    checks = check_points(iterations, f, b)
+    it = 0
+    for c in checks + [iterations - 1]:
+        if c < it:
+            continue
+        model.make_iterations(c - it + 1)
+        for i in range(it, c + 1):
+            out("· Iteration " + str(i))
+        it = c + 1
+        if c in checks:
+            like = model.compute_likelihood()
+            out("· Likelihood " + str(c + 1) + " is " + str(like))
+            if math.fabs((like - like0) / like0) < 0.01:
+                out("\n\t**************************\n\t* Likelihood has converged *\n\t**************************")
+                model.to_file(outfile)
+                return it, True
+            like0 = like
+        if it >= iterations:
+            break
+    return it, False
+
+
+DEFAULTS = {"iterations": 10000, "samples": 100, "sample_ini": 0, "fcheck": 25, "bcheck": 100,
+            "train": "train0.dat", "test": "test0.dat", "out": "", "k": 1, "seed": None}
+
+
+def main(argv=None, model_factory=None, out=print):
+    cfg = dict(DEFAULTS)
+    cfg["seed"] = os.getpid()                                    # :1149
+    try:
+        cfg = parse(sys.argv[1:] if argv is None else argv, cfg)
+    except ArgError:
+        return 2
+    if cfg.get("help"):
+        return 0
+    random.seed(cfg["seed"])
+    if int(cfg["fcheck"]) > int(cfg["iterations"]):
+        out("\n\nWARNING: the likelihood frequency checking is bigger that the number of num_iterations "
+            "per sample.")
+        out("likelihood will only be calculated at the end of every sample (equivalent to --check=0 or -c 0)\n")
+    msg = ("\n****************************************\n* Trigenic Interaction Predictor (MI355X) *"
+           "\n****************************************\n\nDoing " + str(cfg["samples"]) + " samples of "
+           + str(cfg["iterations"]) + " num_iterations.\nTrain-file is " + str(cfg["train"])
+           + "\n Test-file is " + str(cfg["test"]) + "\n Output directory is " + str(cfg["out"])
+           + "\nK value (number of groups) is " + str(cfg["k"]) + ".\nLikelihood will be computed every "
+           + str(cfg["fcheck"]) + " num_iterations after iteration number " + str(cfg["bcheck"]))
+    out(msg)
+    if model_factory is None:
+        from .model import Model as model_factory
+    model = model_factory()
+    model.get_traintest(cfg["train"], cfg["test"])
+    out("\nStarting algorithm...")
+    for sample in range(cfg["sample_ini"], cfg["sample_ini"] + int(cfg["samples"])):
+        outfile = cfg["out"] + "Sample_" + str(sample) + "_K" + str(cfg["k"]) + ".csv"
+        if os.path.isfile(outfile):                              # :1256-1257
+            continue
+        run_sample(model, cfg, sample, outfile, out)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1959,6 +1959,34 @@ int mmsbm_timing(mmsbm_ctx* c, int32_t stride) {
   return MMSBM_OK;
 }
 
+int mmsbm_time_estep(mmsbm_ctx* c, double* theta, double* pr, int32_t n, void* stream,
+                     double* avg_ms) {
+  if (!c || !theta || !pr || !avg_ms || n < 1) return fail(MMSBM_ERR_INVALID, "bad arguments");
+  int rc = check_shape(c);
+  if (rc) return rc;
+  if (!c->genes_set || !c->ws) return fail(MMSBM_ERR_INVALID, "links / workspace not set");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  const Launch& L = kTable[c->K - 1];
+  const bool fused = L.fused && c->estep_variant == 0;
+  c->theta_mut = theta;
+  c->pr_mut = pr;
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, s));
+  for (int i = 0; i < n && rc == MMSBM_OK; ++i) rc = fused ? L.emx(c, s) : L.estep(c, s);
+  HIP_TRY(hipEventRecord(e1, s));
+  HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc) return rc;
+  *avg_ms = (double)ms / n;
+  return MMSBM_OK;
+}
+
 int mmsbm_timing_result(mmsbm_ctx* c, int32_t kernel, double* total_ms, int64_t* count) {
   if (!c || !total_ms || !count) return fail(MMSBM_ERR_INVALID, "null argument");
   if (kernel < 0 || kernel > 2) return fail(MMSBM_ERR_INVALID, "kernel id %d", kernel);

@@ -131,6 +131,13 @@ class EMEngine:
         _lib.check(self.lib.mmsbm_fused(self.ctx, ctypes.byref(v)))
         return bool(v.value)
 
+    def time_estep(self, n: int = 50, stream=None) -> float:
+        """Average device ms of n back-to-back E-step launches (measurement; parameters unchanged)."""
+        ms = ctypes.c_double()
+        _lib.check(self.lib.mmsbm_time_estep(self.ctx, _ptr(self.theta), _ptr(self.pr), int(n),
+                                             _stream(stream), ctypes.byref(ms)))
+        return ms.value
+
     def timing(self, stride: int = 1):
         """Record HIP event pairs around the kernels of every `stride`-th iteration (0: off)."""
         _lib.check(self.lib.mmsbm_timing(self.ctx, int(stride)))
