@@ -71,7 +71,7 @@ def test_layout_rows_and_padding():
     links = {"0_1_2": [1, 0], "10_2_9": [0, 2], "3_3_4": [2, 1], "1_5_6": [0, 1]}
     ids, counts = links_to_arrays(links)
     assert ids[1].tolist() == [10, 2, 9]         # string-sorted key order is kept
-    lay = build_obs(ids, counts)
+    lay = build_obs(ids, counts, by_gene=False)
     assert lay.seg[0] == 0 and all(s % TILE == 0 for s in lay.seg)
     real = lay.obs[lay.link_of_row >= 0]
     assert lay.n_obs == 5
@@ -80,6 +80,17 @@ def test_layout_rows_and_padding():
     assert real[:, 3].tolist() == [1, 2, 2, 1, 1]
     pad = lay.obs[lay.link_of_row < 0]
     assert not pad.any()
+
+
+def test_layout_by_gene_orders_each_rating_by_slot0_gene():
+    links = {"0_1_2": [1, 0], "10_2_9": [0, 2], "3_3_4": [2, 1], "1_5_6": [0, 1]}
+    ids, counts = links_to_arrays(links)
+    lay = build_obs(ids, counts)
+    # r = 0: links 0 (gene 0), 2 (gene 3); r = 1: links 3 (gene 1), 2 (gene 3), 1 (gene 10)
+    assert lay.link_of_row[lay.link_of_row >= 0].tolist() == [0, 2, 3, 2, 1]
+    real = lay.obs[lay.link_of_row >= 0]
+    assert real[:, 0].tolist() == [0, 3, 1, 3, 10]
+    assert real[:, 3].tolist() == [1, 2, 1, 1, 2]
 
 
 def test_gene_csr_lists_every_incidence_and_counter():

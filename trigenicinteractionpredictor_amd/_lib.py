@@ -59,6 +59,7 @@ def load(path: str = LIB) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("MMSBM_LIB", path)  # measurement builds (tools/); default: in-tree build
     if not os.path.exists(path):
         raise ImportError("libmmsbm.so not built at %s: run "
                           "`python -m trigenicinteractionpredictor_amd.build`" % path)

@@ -900,6 +900,12 @@ struct SRows {
 // ------------------------------------------------------------------------------------------
 constexpr int XG = 16;  // observations per wave group
 
+// Measurement builds only (-DEMX_AB=mask): bit 0 U-phase MFMAs, 1 W-phase MFMAs, 2 S-phase
+// MFMAs replaced by VALU adds of the same operands; 3 no contribution stores; 4 no KR stores.
+#ifndef EMX_AB
+#define EMX_AB 0
+#endif
+
 template <int K>
 struct XPlan {
   static constexpr int NG = (K + 3) / 4;      // 4-wide blocks of a / b / g
@@ -985,6 +991,8 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
   // the first group's records and theta values are in flight while p_r is staged
   int grp = g0 + wv;
   int4 eA = make_int4(0, 0, 0, 0), eD = eA, qD = eA, nA = eA, nD = eA, nQ = eA;
+  // records: e* = this group, n* = next group (loaded one iteration earlier, i.e. before the
+  // previous group's stores), m* = the group after (loaded at the top of this iteration)
   double aU[NG], tjD[NG], tiD4[NG];  // th_k[oA][4s+hi], th_j[oD][4j+lo], th_i[oD][4j+lo]
   auto load_theta = [&](const int4& a, const int4& d, double (&u)[NG], double (&tj)[NG],
                         double (&ti)[NG]) {
@@ -1002,6 +1010,10 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
     eD = obs[r0 + oD];
     qD = pos[r0 + oD];
     load_theta(eA, eD, aU, tjD, tiD4);
+    const size_t r1 = (size_t)(grp + NW < g1 ? grp + NW : grp) * XG;
+    nA = obs[r1 + oA];
+    nD = obs[r1 + oD];
+    nQ = pos[r1 + oD];
   }
 
   for (int idx = tid; idx < X::P_DBL; idx += NT) {
@@ -1033,12 +1045,13 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
       TI[oD * KP + 4 * s + lo] = tiD4[s];
     }
     const int gn = grp + NW;
-    {  // records of the next group (its theta values are fetched after the U-phase); past the
-       // end the current group is re-read (branch-free, unused)
-      const size_t r1 = (size_t)(gn < g1 ? gn : grp) * XG;
-      nA = obs[r1 + oA];
-      nD = obs[r1 + oD];
-      nQ = pos[r1 + oD];
+    int4 mA, mD, mQ;
+    {  // records of the group after next; past the end the current group is re-read
+      // (branch-free, unused)
+      const size_t r2 = (size_t)(gn + NW < g1 ? gn + NW : grp) * XG;
+      mA = obs[r2 + oA];
+      mD = obs[r2 + oD];
+      mQ = pos[r2 + oD];
     }
     wave_lds_sync();
 
@@ -1060,7 +1073,8 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
 #pragma unroll
       for (int s = 0; s < NG; ++s)
 #pragma unroll
-        for (int bb = 0; bb < NG; ++bb) acc[bb] = mfma4(aU[s], bf[bb][s], acc[bb]);
+        for (int bb = 0; bb < NG; ++bb)
+          acc[bb] = (EMX_AB & 1) ? acc[bb] + aU[s] + bf[bb][s] : mfma4(aU[s], bf[bb][s], acc[bb]);
       const double ta = TI[oD * KP + a];
       double y = 0.0;
 #pragma unroll
@@ -1100,7 +1114,8 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
       if (a < K) {
         const double ct = cA * TI[oA * KP + a];
 #pragma unroll
-        for (int bq = 0; bq < K; ++bq) KRo[a * K + bq] = ct * tj[bq];
+        for (int bq = 0; bq < K; ++bq)
+          if (!(EMX_AB & 16)) KRo[a * K + bq] = ct * tj[bq];
       }
     }
     wave_lds_sync();
@@ -1117,13 +1132,14 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
       const double av = KRo[cell];
       const double* pb = Pw + cell * KP + lo;  // rows >= K^2 are zero (KR is zero there too)
 #pragma unroll
-      for (int u = 0; u < NG; ++u) wacc[u] = mfma4(av, pb[4 * u], wacc[u]);
+      for (int u = 0; u < NG; ++u)
+        wacc[u] = (EMX_AB & 2) ? wacc[u] + av + pb[4 * u] : mfma4(av, pb[4 * u], wacc[u]);
     }
     unsigned long long t3 = tr.now();
     tph[3] += t3 - t2;
 
     // ---- contributions of observation oD: entries 4 j + lo of its three gene-CSR rows
-    {
+    if (!(EMX_AB & 8)) {
       const bool real = qD.x >= 0;  // padding observations write the trash row (nnz)
       double* ri = cb + (size_t)(real ? qD.x : nnz) * K;
       double* rj = cb + (size_t)(real ? qD.y : nnz) * K;
@@ -1158,7 +1174,8 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
         const int cell = 16 * t + oA;
         const double av = KRs[cell < KRW ? cell : 0];  // cells >= K2 feed discarded S entries
 #pragma unroll
-        for (int u = 0; u < NG; ++u) sacc[t][u] = mfma4(av, bS[u], sacc[t][u]);
+        for (int u = 0; u < NG; ++u)
+          sacc[t][u] = (EMX_AB & 4) ? sacc[t][u] + av + bS[u] : mfma4(av, bS[u], sacc[t][u]);
       }
     }
     wave_lds_sync();  // this group's image reads complete before the next group's writes
@@ -1168,6 +1185,9 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
     eA = nA;
     eD = nD;
     qD = nQ;
+    nA = mA;
+    nD = mD;
+    nQ = mQ;
 #pragma unroll
     for (int s = 0; s < NG; ++s) {
       aU[s] = aU2[s];

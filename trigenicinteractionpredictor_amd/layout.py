@@ -44,11 +44,17 @@ class ObsLayout:
     link_of_row: np.ndarray  # int64[n_obs_pad] link index of each row, -1 for padding
 
 
-def build_obs(ids: np.ndarray, counts: np.ndarray, tile: int = TILE) -> ObsLayout:
+def build_obs(ids: np.ndarray, counts: np.ndarray, tile: int = TILE,
+              by_gene: bool = True) -> ObsLayout:
+    """by_gene: within a rating, order the observations by their slot-0 gene (stable): a wave
+    group's slot-0 rows then fall in one stretch of that gene's CSR run and its th_i loads
+    repeat (summation order only; every sum stays fixed-order)."""
     R = counts.shape[1]
     blocks, owners, seg = [], [], [0]
     for r in range(R):
         sel = np.nonzero(counts[:, r] > 0)[0]
+        if by_gene:
+            sel = sel[np.argsort(ids[sel, 0], kind="stable")]
         n = sel.size
         pad = (-n) % tile
         blk = np.zeros((n + pad, 4), dtype=np.int32)
