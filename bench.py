@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="do not time kernels (overhead probe)")
-    ap.add_argument("--roofline-launches", type=int, default=100,
+    ap.add_argument("--roofline-launches", type=int, default=1000,
                     help="back-to-back E-step launches timed for the roofline")
     ap.add_argument("--event-stride", type=int, default=8,
                     help="time the kernels of every n-th iteration with HIP events")
