@@ -1123,18 +1123,25 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
     tph[2] += t2 - t1;
 
     // ---- W-phase: W' = c W for observation oD, g = 4 u + lo
-    double wacc[NG];
+    // two accumulator sets (even / odd k-steps): 2 NG independent MFMA chains in flight
+    double wacc[NG], wacc2[NG];
 #pragma unroll
-    for (int u = 0; u < NG; ++u) wacc[u] = 0.0;
+    for (int u = 0; u < NG; ++u) {
+      wacc[u] = 0.0;
+      wacc2[u] = 0.0;
+    }
 #pragma unroll
     for (int s = 0; s < NC; ++s) {
       const int cell = 4 * s + hi;
       const double av = KRo[cell];
       const double* pb = Pw + cell * KP + lo;  // rows >= K^2 are zero (KR is zero there too)
+      double (&wa)[NG] = (s & 1) ? wacc2 : wacc;
 #pragma unroll
       for (int u = 0; u < NG; ++u)
-        wacc[u] = (EMX_AB & 2) ? wacc[u] + av + pb[4 * u] : mfma4(av, pb[4 * u], wacc[u]);
+        wa[u] = (EMX_AB & 2) ? wa[u] + av + pb[4 * u] : mfma4(av, pb[4 * u], wa[u]);
     }
+#pragma unroll
+    for (int u = 0; u < NG; ++u) wacc[u] += wacc2[u];
     unsigned long long t3 = tr.now();
     tph[3] += t3 - t2;
 
