@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl",
+                    help="collective backend: nccl (= RCCL over xGMI); gloo only to rehearse "
+                         "several ranks sharing one GPU")
     ap.add_argument("--no-events", action="store_true", help="do not time kernels (overhead probe)")
     ap.add_argument("--roofline-launches", type=int, default=1000,
                     help="back-to-back E-step launches timed for the roofline")
@@ -112,12 +115,16 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    coll = dev if args.backend == "nccl" else torch.device("cpu")  # where collectives run
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from trigenicinteractionpredictor_amd import EMEngine, Model
     from trigenicinteractionpredictor_amd.layout import links_to_arrays, build_obs
@@ -164,9 +171,9 @@ def main():
     # roofline; the in-loop events above also time the dependent-launch boundary around it)
     est_b2b_ms = eng.time_estep(args.roofline_launches)
     elapsed = t1 - t0
-    L = torch.from_numpy(eng.loglik(0)).to(dev)
+    L = torch.from_numpy(eng.loglik(0)).to(coll)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         gathered = [torch.empty_like(L) for _ in range(world)]
