@@ -221,8 +221,9 @@ def main():
             "roofline": {"bound": "mfma" if fused else "fp64-valu", "achieved": achieved_tf,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": ("emx_kernel<%d> (E-step + S, FP64 MFMA)" if fused
-                                    else "estep_kernel<%d> (VALU)") % K,
+                         "kernel": {1: "emx_kernel<%d> (E-step + S, FP64 MFMA)",
+                                    2: "eml_kernel<%d> (E-step + S, FP64 MFMA, lean)"}.get(
+                                        eng.fused_kind, "estep_kernel<%d> (VALU)") % K,
                          "avg_launch_us": est_avg_s * 1e6,
                          "algorithmic_flops_per_launch": flops,
                          "hbm": {"achieved": hbm_bytes / est_avg_s / 1e9, "peak": HBM_PEAK_GBS,

@@ -103,9 +103,9 @@ int mmsbm_loglik(mmsbm_ctx *ctx, int32_t which, const double *theta, const doubl
 int mmsbm_predict(mmsbm_ctx *ctx, const int32_t *ids, int64_t n, const double *theta,
                   const double *pr, double *out, void *stream);
 
-/* *fused = 1 when mmsbm_iterate runs the fused FP64-MFMA E-step (E-step and S accumulation in
- * one kernel, then M2), 0 when it runs the VALU E-step + M1 + M2 (MMSBM_ESTEP, or K outside the
- * fused kernel's range). */
+/* *fused != 0 when mmsbm_iterate runs a fused FP64-MFMA E-step (E-step and S accumulation in
+ * one kernel, then M2): 1 = the KR-image kernel (K <= 10), 2 = the lean kernel (K = 11, 12, or
+ * MMSBM_ESTEP=5); 0 when it runs the VALU E-step + M1 + M2 (MMSBM_ESTEP=1/2, or K > 12). */
 int mmsbm_fused(const mmsbm_ctx *ctx, int32_t *fused);
 
 /* Kernel timing for measurement (bench.py): with stride n > 0, mmsbm_iterate records a HIP

@@ -150,6 +150,42 @@ def test_estep_variants_agree(tmp_path, monkeypatch):
         np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
 
 
+@pytest.mark.parametrize("K", [3, 10, 12])
+@pytest.mark.parametrize("groups", ["1", "256"])
+def test_lean_fused_estep_matches_oracle(tmp_path, monkeypatch, K, groups):
+    """MMSBM_ESTEP=5 (fused E-step without the KR image, 3 waves per SIMD) matches the oracle:
+    one workgroup for everything and the default split, ragged last groups, padded lanes."""
+    tr, te = _fold(tmp_path, 300, 5000, seed=40 + K, multi_frac=0.05, both_frac=0.02)
+    monkeypatch.setenv("MMSBM_ESTEP", "5")
+    monkeypatch.setenv("MMSBM_SACC_WGS", groups)
+    m = _gpu_model(tr, te)
+    random.seed(K)
+    m.initialize_parameters(K)
+    theta0, pr0 = np.array(m.theta), np.array(m.pr)
+    m.make_iterations(2)
+    assert m._engine.fused
+    th_o, pr_o, L_o, _ = _oracle_run(m, theta0, pr0, 2)
+    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
+
+
+@pytest.mark.parametrize("K,kind", [(2, 1), (10, 1), (11, 2), (12, 2), (13, 0)])
+def test_default_estep_kernel_choice(tmp_path, K, kind):
+    """Default dispatch: KR-image fused kernel up to K=10, lean fused kernel at K=11/12 (the
+    KR-image kernel only fits 4 waves there), VALU path above; each matches the oracle."""
+    tr, te = _fold(tmp_path, 200, 3000, seed=60 + K, multi_frac=0.05)
+    m = _gpu_model(tr, te)
+    random.seed(K)
+    m.initialize_parameters(K)
+    theta0, pr0 = np.array(m.theta), np.array(m.pr)
+    m.make_iterations(2)
+    assert m._engine.fused_kind == kind
+    th_o, pr_o, _, _ = _oracle_run(m, theta0, pr0, 2)
+    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+
+
 def test_batched_samples_match_single_runs(tmp_path):
     from trigenicinteractionpredictor_amd import EMEngine, Model
     from trigenicinteractionpredictor_amd.layout import links_to_arrays

@@ -1232,6 +1232,246 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Lean fused E-step + S (MMSBM_ESTEP=5, K <= 12): the same MFMA algebra as emx_kernel without
+// the per-wave KR image (EML_NW waves per workgroup, default 8): the W- and S-phase A operands
+// th_i[a] th_j[b] are formed from the theta images (LDS reads and a multiply), c enters W at
+// the store and S through its B operand (c_o th_k[o][g]).  The W-phase k index runs over
+// (a, b = 4 bb + hi) with b padded to KP (th_j is zero there), so every operand address is a
+// lane base plus a constant.  Y is reduced per a (the lane keeps its entries a = 4 j + lo).
+// ------------------------------------------------------------------------------------------
+#ifndef EML_NW
+#define EML_NW 8
+#endif
+template <int K>
+struct XLPlan {
+  static constexpr int NG = (K + 3) / 4, KP = 4 * NG;
+  static constexpr int K2 = K * K, K3 = K * K * K;
+  static constexpr int NC = (K2 + 3) / 4;     // W-phase k-steps over the (a, b) cells
+  static constexpr int NT4 = (K2 + 15) / 16;  // S-phase 16-cell tiles
+  static constexpr int SACC = NT4 * NG;
+  static constexpr int PW_ROWS = K2 + KP;
+  static constexpr int P_DBL = PW_ROWS * KP;
+  static constexpr int IS = KP + 1;           // image row stride (odd: conflict-free)
+  static constexpr int IMG = 3 * XG * IS;     // th_i / th_j / th_k rows of the group
+  static constexpr int NW = EML_NW;
+  static constexpr int NT = 64 * NW;
+  static constexpr int SLOT = IMG > SACC * 64 ? IMG : SACC * 64;
+  static constexpr int LDS_BYTES = (P_DBL + NW * SLOT) * 8;
+  static constexpr bool ON = K >= 2 && K <= 12 && LDS_BYTES <= 160 * 1024;
+};
+
+template <int K>
+__global__ __launch_bounds__(XLPlan<K>::NT) void eml_kernel(
+    const int4* __restrict__ obs, const int4* __restrict__ pos, const double* __restrict__ theta,
+    const double* __restrict__ pr, double* __restrict__ contrib, double* __restrict__ partS,
+    SRows rg, int P, int R, long long nnz, int G, double eps) {
+  using X = XLPlan<K>;
+  constexpr int NG = X::NG, KP = X::KP, K2 = X::K2, K3 = X::K3, NC = X::NC, NT4 = X::NT4;
+  constexpr int IS = X::IS, NW = X::NW, NT = X::NT, SACC = X::SACC;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Pw = smem;  // [K^2 + KP][KP]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* TI = smem + X::P_DBL + wv * X::SLOT;  // [XG][IS]
+  double* TJ = TI + XG * IS;
+  double* TK = TJ + XG * IS;
+  const int hi = lane >> 4, lo = lane & 3;
+  const int oA = lane & 15, oD = 4 * ((lane >> 2) & 3) + hi;
+  const int w = blockIdx.x, b = blockIdx.y;
+  int r = 0;
+  while (r + 1 < R && w >= rg.whi[r]) ++r;  // workgroup-uniform
+  const int nwg = rg.whi[r] - rg.wlo[r], lw = w - rg.wlo[r];
+  const int ng = rg.grp[r + 1] - rg.grp[r];
+  const int g0 = rg.grp[r] + (int)((long long)lw * ng / nwg);
+  const int g1 = rg.grp[r] + (int)((long long)(lw + 1) * ng / nwg);
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+  const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
+  double* __restrict__ cb = contrib + (size_t)b * (nnz + 1) * K;
+
+  int grp = g0 + wv;
+  // records kept field by field: k gene of oA; i, j genes, weight and CSR rows of oD
+  int kA = 0, iD = 0, jD = 0, nD = 0, q0 = -1, q1 = -1, q2 = -1;
+  int kA2 = 0, iD2 = 0, jD2 = 0, nD2 = 0, q02 = -1, q12 = -1, q22 = -1;
+  double aU[NG], tjD[NG], tiD4[NG];
+  auto load_theta = [&](int k_a, int i_d, int j_d, double (&u)[NG], double (&tj)[NG],
+                        double (&ti)[NG]) {
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      const int g = 4 * s + hi, v = 4 * s + lo;
+      u[s] = g < K ? th[(size_t)k_a * K + g] : 0.0;
+      tj[s] = v < K ? th[(size_t)j_d * K + v] : 0.0;
+      ti[s] = v < K ? th[(size_t)i_d * K + v] : 0.0;
+    }
+  };
+  if (grp < g1) {
+    const size_t r0 = (size_t)grp * XG;
+    const int4 a = obs[r0 + oA], d = obs[r0 + oD], q = pos[r0 + oD];
+    kA = a.z; iD = d.x; jD = d.y; nD = d.w; q0 = q.x; q1 = q.y; q2 = q.z;
+    load_theta(kA, iD, jD, aU, tjD, tiD4);
+  }
+  for (int idx = tid; idx < X::P_DBL; idx += NT) {
+    const int g = idx % KP, row = idx / KP;
+    Pw[idx] = (g < K && row < K2) ? p[row * K + g] : 0.0;
+  }
+  __syncthreads();
+
+  double sacc[NT4][NG];
+#pragma unroll
+  for (int t = 0; t < NT4; ++t)
+#pragma unroll
+    for (int u = 0; u < NG; ++u) sacc[t][u] = 0.0;
+
+  while (grp < g1) {
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      TK[oA * IS + 4 * s + hi] = aU[s];
+      TJ[oD * IS + 4 * s + lo] = tjD[s];
+      TI[oD * IS + 4 * s + lo] = tiD4[s];
+    }
+    const int gn = grp + NW;
+    {
+      const size_t r1 = (size_t)(gn < g1 ? gn : grp) * XG;
+      const int4 a = obs[r1 + oA], d = obs[r1 + oD], q = pos[r1 + oD];
+      kA2 = a.z; iD2 = d.x; jD2 = d.y; nD2 = d.w; q02 = q.x; q12 = q.y; q22 = q.z;
+    }
+    wave_lds_sync();
+
+    // ---- U-phase (Y reduced per a; the lane keeps a = 4 j + lo)
+    double ysel[NG], zp[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      ysel[j] = 0.0;
+      zp[j] = 0.0;
+    }
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+      double bf[NG][NG];
+#pragma unroll
+      for (int bb = 0; bb < NG; ++bb)
+#pragma unroll
+        for (int s = 0; s < NG; ++s) bf[bb][s] = Pw[(a * K + 4 * bb + lo) * KP + 4 * s + hi];
+      double acc[NG];
+#pragma unroll
+      for (int bb = 0; bb < NG; ++bb) acc[bb] = 0.0;
+#pragma unroll
+      for (int s = 0; s < NG; ++s)
+#pragma unroll
+        for (int bb = 0; bb < NG; ++bb) acc[bb] = mfma4(aU[s], bf[bb][s], acc[bb]);
+      const double ta = TI[oD * IS + a];
+      double y = 0.0;
+#pragma unroll
+      for (int bb = 0; bb < NG; ++bb) {
+        y = fma(tjD[bb], acc[bb], y);
+        zp[bb] = fma(ta, acc[bb], zp[bb]);
+      }
+      y += quad_perm<0xB1>(y);
+      y += quad_perm<0x4E>(y);
+      if (lo == (a & 3)) ysel[a >> 2] = y;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    double aU2[NG], tjD2[NG], tiD42[NG];
+    load_theta(kA2, iD2, jD2, aU2, tjD2, tiD42);
+
+    // ---- W-phase: A = th_i[a] th_j[b] of oA, k = (a, b = 4 bb + hi) with b padded to KP
+    //      (th_j = 0 there), B = p[a][b][g]
+    double wacc[NG], tjA[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      tjA[j] = TJ[oA * IS + 4 * j + hi];
+      wacc[j] = 0.0;
+    }
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+      const double tia = TI[oA * IS + a];
+#pragma unroll
+      for (int bb = 0; bb < NG; ++bb) {
+        const double av = tia * tjA[bb];
+        const double* pb = Pw + (a * K + 4 * bb + hi) * KP + lo;
+#pragma unroll
+        for (int u = 0; u < NG; ++u) wacc[u] = mfma4(av, pb[4 * u], wacc[u]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    double dsum = 0.0;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) dsum = fma(tjD[j], zp[j], dsum);
+    dsum += quad_perm<0xB1>(dsum);
+    dsum += quad_perm<0x4E>(dsum);
+    const double c = (double)nD / (dsum + eps);
+
+    // ---- contributions of observation oD: entries 4 j + lo of its three gene-CSR rows
+    {
+      const bool real = q0 >= 0;
+      double* ri = cb + (size_t)(real ? q0 : nnz) * K;
+      double* rj = cb + (size_t)(real ? q1 : nnz) * K;
+      double* rk = cb + (size_t)(real ? q2 : nnz) * K;
+      double* trash = cb + (size_t)nnz * K;
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        const int v = 4 * j + lo;
+        const int vs = v < K ? v : K - 1;
+        (v < K ? ri : trash)[vs] = c * ysel[j];
+        (v < K ? rj : trash)[vs] = c * zp[j];
+        (v < K ? rk : trash)[vs] = c * wacc[j];
+      }
+    }
+
+    // ---- S-phase: A = th_i th_j of o = 4 s + hi at cell 16 t + oA, B = c_o th_k[o].  The
+    //      image bases pass through an empty asm each group: the per-(s, t) addresses are then
+    //      formed in the loop as base + offset(t) with s folded into the instruction offset,
+    //      instead of 8 NT4 loop-invariant registers.
+    int zb = 0, oAv = oA;
+    asm volatile("" : "+v"(zb), "+v"(oAv));
+    const double* TIs = TI + zb + hi * IS;
+    const double* TJs = TJ + zb + hi * IS;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int o = 4 * s + hi;
+      const double co = __shfl(c, 16 * (o & 3) + 4 * (o >> 2), 64);
+      double bS[NG];
+#pragma unroll
+      for (int u = 0; u < NG; ++u) bS[u] = co * TK[o * IS + 4 * u + lo];
+#pragma unroll
+      for (int t = 0; t < NT4; ++t) {
+        const int cell = 16 * t + oAv;
+        const int cc = cell < K2 ? cell : K2 - 1;  // cells >= K2 feed discarded S entries
+        const double av = TIs[cc / K + 4 * s * IS] * TJs[cc % K + 4 * s * IS];
+#pragma unroll
+        for (int u = 0; u < NG; ++u) sacc[t][u] = mfma4(av, bS[u], sacc[t][u]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wave_lds_sync();
+    kA = kA2; iD = iD2; jD = jD2; nD = nD2; q0 = q02; q1 = q12; q2 = q22;
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      aU[s] = aU2[s];
+      tjD[s] = tjD2[s];
+      tiD4[s] = tiD42[s];
+    }
+    grp = gn;
+  }
+
+  __syncthreads();
+  double* red = smem + X::P_DBL;  // wave q's accumulators at red + q * SLOT, [SACC][64]
+#pragma unroll
+  for (int t = 0; t < NT4; ++t)
+#pragma unroll
+    for (int u = 0; u < NG; ++u) red[wv * X::SLOT + (t * NG + u) * 64 + lane] = sacc[t][u];
+  __syncthreads();
+  double* __restrict__ rowS = partS + ((size_t)b * G + w) * K3;
+  for (int idx = tid; idx < SACC * 64; idx += NT) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += red[q * X::SLOT + idx];
+    const int t = idx >> 6, ln = idx & 63;
+    const int cell = 16 * (t / NG) + 4 * ((ln >> 2) & 3) + (ln >> 4);
+    const int g = 4 * (t % NG) + (ln & 3);
+    if (cell < K2 && g < K) rowS[cell * K + g] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // M2, grid (p_blocks + P, B), block 256.
 //  blocks [0, p_blocks): p (:1021-1028), 8 cells x 32 row slices per block.  Partial row n
 //    (n < NR = G * rs) sits at partS + (b * NR + n) * K3 and belongs to rating n % R (M1
@@ -1459,6 +1699,7 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Launch {
   bool fused;  // emx_kernel compiled for this K
+  bool lean;   // eml_kernel is the default fused kernel for this K
   int (*emx)(mmsbm_ctx*, hipStream_t);
   int (*estep)(mmsbm_ctx*, hipStream_t);
   int (*m1)(mmsbm_ctx*, hipStream_t);
@@ -1630,8 +1871,45 @@ int launch_m1(mmsbm_ctx* c, hipStream_t s) {
   return MMSBM_OK;
 }
 
+// Fused kernel choice: MMSBM_ESTEP=5 forces the lean kernel; by default it runs where the
+// KR-image kernel only fits 4 waves per workgroup (K = 11, 12: measured 14-16 % faster there).
+template <int K>
+constexpr bool lean_default() {
+  return XLPlan<K>::ON && (!XPlan<K>::ON || XPlan<K>::NW < 8);
+}
+template <int K>
+bool use_lean(int variant) {
+  return XLPlan<K>::ON && (variant == 5 || (variant == 0 && lean_default<K>()));
+}
+
+template <int K>
+int launch_eml(mmsbm_ctx* c, hipStream_t s) {
+  if constexpr (XLPlan<K>::ON) {
+    const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
+    if (tr.ntiles == 0) return MMSBM_OK;
+    int G = 1;
+    const SRows rg = fused_rows(c, &G);
+    static bool attr = false;
+    if (!attr) {
+      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&eml_kernel<K>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, XLPlan<K>::LDS_BYTES));
+      attr = true;
+    }
+    eml_kernel<K><<<dim3(G, c->B), XLPlan<K>::NT, XLPlan<K>::LDS_BYTES, s>>>(
+        tr.obs, reinterpret_cast<const int4*>(c->pos), c->theta_mut, c->pr_mut, c->contrib,
+        c->partS, rg, c->P, c->R, c->nnz, G, c->eps);
+    HIP_TRY(hipGetLastError());
+    return MMSBM_OK;
+  } else {
+    return fail(MMSBM_ERR_UNSUPPORTED, "lean fused E-step not compiled for K=%d", K);
+  }
+}
+
 template <int K>
 int launch_emx(mmsbm_ctx* c, hipStream_t s) {
+  if constexpr (XLPlan<K>::ON) {
+    if (use_lean<K>(c->estep_variant)) return launch_eml<K>(c, s);
+  }
   if constexpr (XPlan<K>::ON) {
     const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
     if (tr.ntiles == 0) return MMSBM_OK;
@@ -1698,7 +1976,7 @@ int launch_predict(mmsbm_ctx* c, const int* ids, long long n, const double* thet
 template <int... Ks>
 constexpr auto make_table(std::integer_sequence<int, Ks...>) {
   return std::array<Launch, sizeof...(Ks)>{
-      Launch{XPlan<Ks + 1>::ON, &launch_emx<Ks + 1>, &launch_estep<Ks + 1>, &launch_m1<Ks + 1>,
+      Launch{XPlan<Ks + 1>::ON, lean_default<Ks + 1>(), &launch_emx<Ks + 1>, &launch_estep<Ks + 1>, &launch_m1<Ks + 1>,
              &launch_m2<Ks + 1>, &launch_loglik<Ks + 1>, &launch_predict<Ks + 1>}...};
 }
 
@@ -1902,7 +2180,7 @@ int mmsbm_iterate(mmsbm_ctx* c, double* theta, double* pr, int32_t n_iters, void
   const Launch& L = kTable[c->K - 1];
   c->theta_mut = theta;
   c->pr_mut = pr;
-  const bool fused = L.fused && c->estep_variant == 0;
+  const bool fused = L.fused && (c->estep_variant == 0 || c->estep_variant == 5);
   for (int it = 0; it < n_iters; ++it) {
     const bool mark = c->timing && (it % c->timing_stride == 0);
     if (mark && (rc = timing_mark(c, 0, s))) return rc;
@@ -1974,7 +2252,9 @@ int mmsbm_fused(const mmsbm_ctx* c, int32_t* fused) {
   if (!c || !fused) return fail(MMSBM_ERR_INVALID, "null argument");
   int rc = check_shape(c);
   if (rc) return rc;
-  *fused = kTable[c->K - 1].fused && c->estep_variant == 0 ? 1 : 0;
+  const Launch& L = kTable[c->K - 1];
+  const bool on = L.fused && (c->estep_variant == 0 || c->estep_variant == 5);
+  *fused = !on ? 0 : (c->estep_variant == 5 || L.lean) ? 2 : 1;
   return MMSBM_OK;
 }
 
@@ -1995,7 +2275,7 @@ int mmsbm_time_estep(mmsbm_ctx* c, double* theta, double* pr, int32_t n, void* s
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   const Launch& L = kTable[c->K - 1];
-  const bool fused = L.fused && c->estep_variant == 0;
+  const bool fused = L.fused && (c->estep_variant == 0 || c->estep_variant == 5);
   c->theta_mut = theta;
   c->pr_mut = pr;
   hipEvent_t e0, e1;

@@ -127,9 +127,14 @@ class EMEngine:
     @property
     def fused(self) -> bool:
         """True when iterate() runs the fused FP64-MFMA E-step (E-step + S in one kernel)."""
+        return self.fused_kind != 0
+
+    @property
+    def fused_kind(self) -> int:
+        """0 VALU E-step + M1, 1 fused KR-image kernel (emx), 2 fused lean kernel (eml)."""
         v = ctypes.c_int32()
         _lib.check(self.lib.mmsbm_fused(self.ctx, ctypes.byref(v)))
-        return bool(v.value)
+        return int(v.value)
 
     def time_estep(self, n: int = 50, stream=None) -> float:
         """Average device ms of n back-to-back E-step launches (measurement; parameters unchanged)."""
