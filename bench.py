@@ -56,6 +56,11 @@ def parse():
     ap.add_argument("--no-events", action="store_true", help="do not time kernels (overhead probe)")
     ap.add_argument("--roofline-launches", type=int, default=1000,
                     help="back-to-back E-step launches timed for the roofline")
+    ap.add_argument("--shard", choices=("samples", "links"), default="samples",
+                    help="samples: independent restarts per rank (weak scaling, the default); "
+                         "links: ONE batch of samples whose train links are split over the ranks, "
+                         "one all-reduce of the accumulators per iteration (strong scaling, "
+                         "SURVEY.md 8e secondary)")
     ap.add_argument("--event-stride", type=int, default=8,
                     help="time the kernels of every n-th iteration with HIP events")
     return ap.parse_args()
@@ -136,29 +141,40 @@ def main():
         host = Model()
         host.get_traintest(train, test)
     K, B = args.K, args.samples
-    # restart sharding: global sample s = rank*B + b; one RNG stream seeded once, like :1149/:1260
+    links_mode = args.shard == "links"
+    # restart sharding: global sample s = rank*B + b; one RNG stream seeded once, like :1149/:1260.
+    # link sharding: every rank holds the same B samples (s = 0..B-1) and 1/world of the links.
+    first = 0 if links_mode else rank * B
     random.seed(args.seed)
     thetas, prs = [], []
-    for s in range((rank + 1) * B):
+    for s in range(first + B):
         host.initialize_parameters(K)
-        if s >= rank * B:
+        if s >= first:
             thetas.append(np.array(host._theta))
             prs.append(np.array(host._pr))
     eng = EMEngine(K, host.P, B=B, device=dev)
     ids, counts = links_to_arrays(host.links)
-    eng.set_links(0, ids, counts)
-    eng.set_links(1, *links_to_arrays(host.test_links))
-    eng.upload(np.stack(thetas), np.stack(prs))
-    E_obs = int(build_obs(ids, counts).n_obs)
+    tids, tcounts = links_to_arrays(host.test_links)
+    if links_mode:
+        from trigenicinteractionpredictor_amd.linkshard import LinkShardedEM, shard_links
+        runner = LinkShardedEM(eng, ids, counts, tids, tcounts)
+        lo, hi = shard_links(ids.shape[0], world, rank)
+        E_obs = int(build_obs(ids[lo:hi], counts[lo:hi]).n_obs)   # this rank's E-step launch
+    else:
+        eng.set_links(0, ids, counts)
+        eng.set_links(1, tids, tcounts)
+        runner = eng
+        E_obs = int(build_obs(ids, counts).n_obs)
+    runner.upload(np.stack(thetas), np.stack(prs))
 
-    eng.iterate(args.warmup)
+    runner.iterate(args.warmup)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     eng.timing(0 if args.no_events else args.event_stride)
     t0 = time.perf_counter()
-    eng.iterate(args.steps)
+    runner.iterate(args.steps)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
@@ -171,7 +187,7 @@ def main():
     # roofline; the in-loop events above also time the dependent-launch boundary around it)
     est_b2b_ms = eng.time_estep(args.roofline_launches)
     elapsed = t1 - t0
-    L = torch.from_numpy(eng.loglik(0)).to(coll)
+    L = torch.from_numpy(runner.loglik(0)).to(coll)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -183,7 +199,7 @@ def main():
         L_all = L.cpu().numpy()
 
     if rank == 0:
-        iters_total = args.steps * B * world
+        iters_total = args.steps * B * (1 if links_mode else world)
         value = iters_total / elapsed
         # roofline of the dominant kernel (the E-step), per launch; SURVEY.md §8d figures.
         # Fused path (FP64 MFMA): the E-step launch does Y, Z, W and S = 8 K^3 per observation;
@@ -209,13 +225,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if links_mode else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic fold0 stand-in (real fold0 is a Git-LFS pointer)",
-            "config": {"workload": "fold0 stand-in, K=%d, %d sample(s)/GPU" % (K, B), "K": K,
+            "config": {"workload": ("fold0 stand-in, K=%d, %d sample(s) link-sharded over %d GPU(s)"
+                                    % (K, B, world)) if links_mode else
+                                   "fold0 stand-in, K=%d, %d sample(s)/GPU" % (K, B), "K": K,
                        "P": host.P, "E_train": len(host.links), "E_test": len(host.test_links),
-                       "E_obs": E_obs, "samples_per_gpu": B, "parallelism": "restart-sharded x%d" % world},
+                       "E_obs": E_obs, "samples_per_gpu": B,
+                       "parallelism": ("link-sharded x%d" if links_mode else "restart-sharded x%d") % world},
             "final_loglik": float(L_all[0]),
             "final_loglik_best": float(L_all.max()),
             "roofline": {"bound": "mfma" if fused else "fp64-valu", "achieved": achieved_tf,

@@ -103,6 +103,19 @@ int mmsbm_loglik(mmsbm_ctx *ctx, int32_t which, const double *theta, const doubl
 int mmsbm_predict(mmsbm_ctx *ctx, const int32_t *ids, int64_t n, const double *theta,
                   const double *pr, double *out, void *stream);
 
+/* Link-sharded iteration (single sample over N ranks): each rank's context
+ * holds 1/N of the train links (mmsbm_set_links) and the GLOBAL degree (mmsbm_set_genes' deg).
+ * Step 1, the accumulation half of make_iteration (:986-1012) over this rank's links:
+ *   nth[B][P][K]   = per gene, the sum of its local c-scaled (Y | Z | W) rows (theta not applied)
+ *   S[B][R][K^3]   = the S lattice sums,  npr = p S.
+ * The caller sums nth and S over ranks (one all-reduce of one buffer), then step 2 applies the
+ * M-step (:1016-1028): theta <- theta nth / deg, p_r <- p_r S_r / (eps + sum_r p_r S_r).
+ * Called on one rank with all links, the pair equals mmsbm_iterate(n = 1). */
+int mmsbm_accumulate(mmsbm_ctx *ctx, const double *theta, const double *pr, double *nth, double *S,
+                     void *stream);
+int mmsbm_mstep(mmsbm_ctx *ctx, double *theta, double *pr, const double *nth, const double *S,
+                void *stream);
+
 /* *fused != 0 when mmsbm_iterate runs a fused FP64-MFMA E-step (E-step and S accumulation in
  * one kernel, then M2): 1 = the KR-image kernel (K <= 10), 2 = the lean kernel (K = 11, 12, or
  * MMSBM_ESTEP=5); 0 when it runs the VALU E-step + M1 + M2 (MMSBM_ESTEP=1/2, or K > 12). */

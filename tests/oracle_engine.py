@@ -29,3 +29,48 @@ class OracleEngine:
 
     def download(self):
         return np.stack(self.theta), np.stack(self.pr)
+
+
+class OracleShardEngine:
+    """CPU stand-in for the link-sharded EMEngine methods (set_links with a global degree,
+    accumulate, mstep) on oracle/shard_oracle.py, B batched samples."""
+
+    def __init__(self, K, P, B=1, R=2, eps=1e-10):
+        self.K, self.P, self.B, self.R, self.eps = K, P, B, R, eps
+        self.device = "cpu"
+        self.sets = {}
+        self.deg = None
+
+    def set_links(self, which, ids, counts, deg=None):
+        self.sets[which] = (np.asarray(ids, np.int32), np.asarray(counts, np.int32))
+        if which == 0:
+            self.deg = np.asarray(deg if deg is not None else
+                                  np.bincount(np.asarray(ids).ravel(), minlength=self.P)[:self.P])
+
+    def upload(self, theta, pr):
+        self.theta = [np.array(t, dtype=np.float64) for t in theta]
+        self.pr = [np.array(p, dtype=np.float64) for p in pr]
+
+    def download(self):
+        return np.stack(self.theta), np.stack(self.pr)
+
+    def accumulate(self, nth, S):
+        import torch
+        from oracle import shard_oracle
+        ids, counts = self.sets[0]
+        for b in range(self.B):
+            n, s = shard_oracle.accumulate(ids, counts, self.theta[b], self.pr[b], self.eps)
+            nth[b].copy_(torch.from_numpy(n))
+            S[b].copy_(torch.from_numpy(s))
+
+    def mstep(self, nth, S):
+        from oracle import shard_oracle
+        for b in range(self.B):
+            self.theta[b], self.pr[b] = shard_oracle.mstep(self.theta[b], self.pr[b], nth[b].numpy(),
+                                                           S[b].numpy(), self.deg, self.eps)
+
+    def loglik(self, which):
+        ids, counts = self.sets[which]
+        if ids.shape[0] == 0:
+            return np.zeros(self.B)
+        return np.array([c_oracle.loglik(ids, counts, t, p) for t, p in zip(self.theta, self.pr)])

@@ -39,6 +39,8 @@ SIGNATURES = {
     "mmsbm_iterate": (_c_int, [_vp, _vp, _vp, _c_i32, _vp]),
     "mmsbm_loglik": (_c_int, [_vp, _c_i32, _vp, _vp, _vp, _vp]),
     "mmsbm_predict": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _vp, _vp]),
+    "mmsbm_accumulate": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmsbm_mstep": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "mmsbm_fused": (_c_int, [_vp, ctypes.POINTER(_c_i32)]),
     "mmsbm_timing": (_c_int, [_vp, _c_i32]),
     "mmsbm_time_estep": (_c_int, [_vp, _vp, _vp, _c_i32, _vp, ctypes.POINTER(_c_dbl)]),

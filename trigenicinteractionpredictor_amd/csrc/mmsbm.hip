@@ -1492,7 +1492,9 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
                                                  const int* __restrict__ gptr,
                                                  const int* __restrict__ deg, SRows rg, int P,
                                                  int R, int G, long long nnz, int p_blocks,
-                                                 double eps, int ablate) {
+                                                 double eps, int ablate,
+                                                 double* __restrict__ nth_out,
+                                                 double* __restrict__ S_out) {
   constexpr int K3 = K * K * K;
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
@@ -1521,8 +1523,12 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
       double sum = 0.0;
 #pragma unroll
       for (int q = 0; q < NS; ++q) sum += tred[q * K + tid];
-      double* row = theta + (size_t)b * P * K + (size_t)g * K;
-      row[tid] = row[tid] * sum / (double)deg[g];
+      if (nth_out) {  // link-sharded: this rank's sum, applied after the cross-rank reduction
+        nth_out[(size_t)b * P * K + (size_t)g * K + tid] = sum;
+      } else {
+        double* row = theta + (size_t)b * P * K + (size_t)g * K;
+        row[tid] = row[tid] * sum / (double)deg[g];
+      }
     }
     return;
   }
@@ -1565,7 +1571,14 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
   for (int q = 0; q < MAX_R; ++q)
     if (q < R) red[q][sl][cl] = acc[q];
   __syncthreads();
-  if (sl == 0 && cell < K3) {
+  if (sl == 0 && cell < K3 && S_out) {  // link-sharded: this rank's S sums
+    for (int q = 0; q < R; ++q) {
+      double s = 0.0;
+#pragma unroll
+      for (int z = 0; z < MP_SLICES; ++z) s += red[q][z][cl];
+      S_out[((size_t)b * R + q) * K3 + cell] = s;
+    }
+  } else if (sl == 0 && cell < K3) {
     double npr[MAX_R];
     double den = eps;
     double* pc = pr + (size_t)b * R * K3 + cell;
@@ -1574,6 +1587,40 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
 #pragma unroll
       for (int z = 0; z < MP_SLICES; ++z) s += red[q][z][cl];
       npr[q] = pc[(size_t)q * K3] * s;
+      den += npr[q];
+    }
+    for (int q = 0; q < R; ++q) pc[(size_t)q * K3] = npr[q] / den;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// M-step from summed accumulators (link-sharded iteration, after the cross-rank all-reduce):
+//   theta[g][a] <- theta[g][a] * nth[g][a] / deg[g]                          (:1016-1018)
+//   p_r <- p_r S_r / (eps + sum_r p_r S_r)                                      (:1021-1028)
+// with the same operation order as m2_kernel.  Grid (ceil((P K + K^3) / 256), B).
+// ------------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void mapply_kernel(double* __restrict__ theta, double* __restrict__ pr,
+                                                     const double* __restrict__ nth,
+                                                     const double* __restrict__ S,
+                                                     const int* __restrict__ deg, int P, int R,
+                                                     double eps) {
+  constexpr int K3 = K * K * K;
+  const int b = blockIdx.y;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long PK = (long long)P * K;
+  if (idx < PK) {
+    const int g = (int)(idx / K);
+    double* t = theta + (size_t)b * PK + idx;
+    *t = *t * nth[(size_t)b * PK + idx] / (double)deg[g];
+  } else if (idx < PK + K3) {
+    const int cell = (int)(idx - PK);
+    double npr[MAX_R];
+    double den = eps;
+    double* pc = pr + (size_t)b * R * K3 + cell;
+    const double* sc = S + (size_t)b * R * K3 + cell;
+    for (int q = 0; q < R; ++q) {
+      npr[q] = pc[(size_t)q * K3] * sc[(size_t)q * K3];
       den += npr[q];
     }
     for (int q = 0; q < R; ++q) pc[(size_t)q * K3] = npr[q] / den;
@@ -1704,6 +1751,7 @@ struct Launch {
   int (*estep)(mmsbm_ctx*, hipStream_t);
   int (*m1)(mmsbm_ctx*, hipStream_t);
   int (*m2)(mmsbm_ctx*, hipStream_t, bool);
+  int (*mapply)(mmsbm_ctx*, double*, double*, const double*, const double*, hipStream_t);
   int (*loglik)(mmsbm_ctx*, int, const double*, const double*, hipStream_t);
   int (*predict)(mmsbm_ctx*, const int*, long long, const double*, const double*, double*,
                  hipStream_t);
@@ -1729,6 +1777,8 @@ struct mmsbm_ctx {
   double* cvec = nullptr;
   double* partS = nullptr;
   double* partL = nullptr;
+  double* nth_out = nullptr;  // set only inside mmsbm_accumulate (link-sharded sums)
+  double* S_out = nullptr;
   // current iterate (only valid during a call)
   double* theta_mut = nullptr;
   double* pr_mut = nullptr;
@@ -1936,7 +1986,13 @@ template <int K>
 int launch_m2(mmsbm_ctx* c, hipStream_t s, bool fused) {
   constexpr int K3 = K * K * K;
   const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
-  if (tr.ntiles == 0) return MMSBM_OK;
+  if (tr.ntiles == 0) {
+    if (c->nth_out) {  // a rank without train links contributes zeros
+      HIP_TRY(hipMemsetAsync(c->nth_out, 0, sizeof(double) * c->B * c->P * K, s));
+      HIP_TRY(hipMemsetAsync(c->S_out, 0, sizeof(double) * c->B * c->R * K3, s));
+    }
+    return MMSBM_OK;
+  }
   int G = sacc_groups(c);
   SRows rg;
   if (fused)
@@ -1947,7 +2003,17 @@ int launch_m2(mmsbm_ctx* c, hipStream_t s, bool fused) {
   const int theta_blocks = c->P;  // one workgroup per gene
   m2_kernel<K><<<dim3(p_blocks + theta_blocks, c->B), 256, 0, s>>>(
       c->pr_mut, c->theta_mut, c->partS, c->contrib, c->gptr, c->deg, rg, c->P, c->R, G,
-      c->nnz, p_blocks, c->eps, c->ablate);
+      c->nnz, p_blocks, c->eps, c->ablate, c->nth_out, c->S_out);
+  HIP_TRY(hipGetLastError());
+  return MMSBM_OK;
+}
+
+template <int K>
+int launch_mapply(mmsbm_ctx* c, double* theta, double* pr, const double* nth, const double* S,
+                  hipStream_t s) {
+  const long long n = (long long)c->P * K + (long long)K * K * K;
+  mapply_kernel<K><<<dim3((unsigned)((n + 255) / 256), c->B), 256, 0, s>>>(theta, pr, nth, S, c->deg,
+                                                                           c->P, c->R, c->eps);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -1977,7 +2043,7 @@ template <int... Ks>
 constexpr auto make_table(std::integer_sequence<int, Ks...>) {
   return std::array<Launch, sizeof...(Ks)>{
       Launch{XPlan<Ks + 1>::ON, lean_default<Ks + 1>(), &launch_emx<Ks + 1>, &launch_estep<Ks + 1>, &launch_m1<Ks + 1>,
-             &launch_m2<Ks + 1>, &launch_loglik<Ks + 1>, &launch_predict<Ks + 1>}...};
+             &launch_m2<Ks + 1>, &launch_mapply<Ks + 1>, &launch_loglik<Ks + 1>, &launch_predict<Ks + 1>}...};
 }
 
 const auto kTable = make_table(std::make_integer_sequence<int, MMSBM_MAX_K>{});
@@ -2213,6 +2279,45 @@ int mmsbm_iterate(mmsbm_ctx* c, double* theta, double* pr, int32_t n_iters, void
             sum[6] / nw, sum[7] / nw, sum[8] / nw, mx);
   }
   return MMSBM_OK;
+}
+
+int mmsbm_accumulate(mmsbm_ctx* c, const double* theta, const double* pr, double* nth, double* S,
+                     void* stream) {
+  if (!c) return fail(MMSBM_ERR_INVALID, "null context");
+  int rc = check_shape(c);
+  if (rc) return rc;
+  if (!c->genes_set) return fail(MMSBM_ERR_INVALID, "call mmsbm_set_genes first");
+  if (!c->ws || c->ws_bytes < (long long)ws_layout(c).total)
+    return fail(MMSBM_ERR_INVALID, "workspace missing or too small");
+  if (!theta || !pr || !nth || !S) return fail(MMSBM_ERR_INVALID, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  const Launch& L = kTable[c->K - 1];
+  // the E-step kernels only read theta / pr; m2 in sums-out mode writes nth / S, not them
+  c->theta_mut = const_cast<double*>(theta);
+  c->pr_mut = const_cast<double*>(pr);
+  const bool fused = L.fused && (c->estep_variant == 0 || c->estep_variant == 5);
+  if ((rc = fused ? L.emx(c, s) : L.estep(c, s))) return rc;
+  if (!fused && (rc = L.m1(c, s))) return rc;
+  c->nth_out = nth;
+  c->S_out = S;
+  rc = L.m2(c, s, fused);
+  c->nth_out = nullptr;
+  c->S_out = nullptr;
+  return rc;
+}
+
+int mmsbm_mstep(mmsbm_ctx* c, double* theta, double* pr, const double* nth, const double* S,
+                void* stream) {
+  if (!c) return fail(MMSBM_ERR_INVALID, "null context");
+  int rc = check_shape(c);
+  if (rc) return rc;
+  if (!c->genes_set) return fail(MMSBM_ERR_INVALID, "call mmsbm_set_genes first");
+  if (c->zero_degree)
+    return fail(MMSBM_ERR_ZERO_DEGREE, "a gene has no train link (float division by zero)");
+  if (!theta || !pr || !nth || !S) return fail(MMSBM_ERR_INVALID, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  return kTable[c->K - 1].mapply(c, theta, pr, nth, S, (hipStream_t)stream);
 }
 
 int mmsbm_loglik(mmsbm_ctx* c, int32_t which, const double* theta, const double* pr, double* out,

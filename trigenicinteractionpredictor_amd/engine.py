@@ -50,7 +50,9 @@ class EMEngine:
     def _dev(self, a: np.ndarray) -> torch.Tensor:
         return torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
 
-    def set_links(self, which: int, ids: np.ndarray, counts: np.ndarray):
+    def set_links(self, which: int, ids: np.ndarray, counts: np.ndarray, deg: np.ndarray = None):
+        """deg: the reference's `counter` over ALL train links; defaults to the one of `ids`
+        (a link-sharded rank passes the global one)."""
         lay = build_obs(ids, counts, TILE)
         obs_d = self._dev(lay.obs)
         seg = (ctypes.c_int64 * (self.R + 1))(*[int(x) for x in lay.seg])
@@ -59,6 +61,8 @@ class EMEngine:
         self._sets[which] = (lay, obs_d)
         if which == _lib.SET_TRAIN:
             csr = build_gene_csr(lay, ids, self.P)
+            if deg is not None:
+                csr.deg = np.ascontiguousarray(deg, dtype=np.int32)
             ptr_d, inc_d, deg_d = self._dev(csr.ptr), self._dev(csr.inc), self._dev(csr.deg)
             self._csr = (csr, ptr_d, inc_d, deg_d)
             rc = self.lib.mmsbm_set_genes(self.ctx, _ptr(ptr_d), _ptr(inc_d) if inc_d.numel() else None,
@@ -98,6 +102,20 @@ class EMEngine:
             raise RuntimeError("train links not set")
         _lib.check(self.lib.mmsbm_iterate(self.ctx, _ptr(self.theta), _ptr(self.pr), int(n_iters),
                                           _stream(stream)))
+
+    def accumulate(self, nth: torch.Tensor, S: torch.Tensor, stream=None):
+        """Link-sharded step 1 (include/mmsbm.h): this context's sums nth [B][P][K], S [B][R][K^3]."""
+        if _lib.SET_TRAIN not in self._sets:
+            raise RuntimeError("train links not set")
+        _lib.check(self.lib.mmsbm_accumulate(self.ctx, _ptr(self.theta), _ptr(self.pr), _ptr(nth),
+                                             _ptr(S), _stream(stream)))
+
+    def mstep(self, nth: torch.Tensor, S: torch.Tensor, stream=None):
+        """Link-sharded step 2: M-step from the summed nth / S (ZeroDivisionError like :1018)."""
+        if self.zero_degree:
+            raise ZeroDivisionError("float division by zero")
+        _lib.check(self.lib.mmsbm_mstep(self.ctx, _ptr(self.theta), _ptr(self.pr), _ptr(nth), _ptr(S),
+                                        _stream(stream)))
 
     def loglik_async(self, which: int = _lib.SET_TRAIN, out: torch.Tensor = None, stream=None):
         if out is None:
