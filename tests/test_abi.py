@@ -62,3 +62,14 @@ def test_no_cpu_fallback_in_product_path():
             if f.endswith(".py"):
                 src = open(os.path.join(root, f)).read()
                 assert "oracle" not in re.sub(r"#.*", "", src).replace('"""', ""), f
+
+
+def test_ingest_library_exports_its_header():
+    """include/mmsbm_io.h (host fold reader) is exported by libmmsbm_io.so."""
+    from trigenicinteractionpredictor_amd import build
+    text = open(os.path.join(REPO, "include", "mmsbm_io.h")).read()
+    syms = sorted(set(re.findall(r"^\s*(?:int|void)\s*(mmsbm_\w+)\s*\(", text, re.M)))
+    assert syms == ["mmsbm_fold_export", "mmsbm_fold_free", "mmsbm_fold_parse", "mmsbm_fold_sizes"]
+    lib = ctypes.CDLL(build.build_io(verbose=False))
+    for name in syms:
+        assert hasattr(lib, name), name

@@ -16,6 +16,8 @@ SRC = os.path.join(PKG, "csrc", "mmsbm.hip")
 INCLUDE = os.path.join(REPO, "include")
 OUT_DIR = os.path.join(PKG, "_build")
 LIB = os.path.join(OUT_DIR, "libmmsbm.so")
+SRC_IO = os.path.join(PKG, "csrc", "fold_io.cpp")
+LIB_IO = os.path.join(OUT_DIR, "libmmsbm_io.so")  # host-only ingestion (include/mmsbm_io.h)
 ARCH = os.environ.get("MMSBM_OFFLOAD_ARCH", "gfx950")
 
 
@@ -52,5 +54,23 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
+def build_io(force: bool = False, verbose: bool = True) -> str:
+    """Host C++ fold reader (no GPU code): g++ -O2."""
+    deps = [SRC_IO, os.path.join(INCLUDE, "mmsbm_io.h")]
+    if not force and os.path.exists(LIB_IO) and all(os.path.getmtime(d) <= os.path.getmtime(LIB_IO)
+                                                     for d in deps):
+        return LIB_IO
+    os.makedirs(OUT_DIR, exist_ok=True)
+    tmp = LIB_IO + ".tmp"
+    cmd = [shutil.which("g++") or "g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I" + INCLUDE,
+           "-o", tmp, SRC_IO]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB_IO)
+    return LIB_IO
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_io(force="--force" in sys.argv)

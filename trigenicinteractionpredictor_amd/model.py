@@ -25,8 +25,13 @@ from . import _lib
 from .layout import links_to_arrays
 
 
+NATIVE_INGEST = True   # get_traintest's native reader for canonical files (ingest.py)
+
+
 class Model:
     def __init__(self, device=None):
+        self._fold = None               # native parse backing the lazy link dicts (ingest.py)
+        self._fold_fresh = [False, False]
         self.ntheta = []
         self._theta = []
         self.id_gene = {}
@@ -85,6 +90,56 @@ class Model:
         self._pr = value
         self._dev_fresh = False
 
+    # ---------------------------------------------- link tables (lazy after a native parse)
+    # After get_traintest's native reader, `links` / `nlinks` / `test_links` are built as the
+    # reference's dicts on first access; until a caller has touched them the engine and the
+    # counts below read the parsed arrays directly.
+    @property
+    def links(self):
+        if self._links is None:
+            self._links = self._fold.links_dict()
+        self._fold_fresh[0] = False     # the caller may edit the dict
+        return self._links
+
+    @links.setter
+    def links(self, value):
+        self._links = value
+        self._fold_fresh[0] = False
+
+    @property
+    def test_links(self):
+        if self._test_links is None:
+            self._test_links = self._fold.test_links_dict()
+        self._fold_fresh[1] = False
+        return self._test_links
+
+    @test_links.setter
+    def test_links(self, value):
+        self._test_links = value
+        self._fold_fresh[1] = False
+
+    @property
+    def nlinks(self):
+        if self._nlinks is None:
+            self._nlinks = self._fold.nlinks_dict()
+        return self._nlinks
+
+    @nlinks.setter
+    def nlinks(self, value):
+        self._nlinks = value
+
+    def _link_arrays(self, which):
+        """(ids int32[E][3] in key order, counts int32[E][R]) of the train (0) / test (1) links."""
+        if self._fold is not None and self._fold_fresh[which]:
+            f = self._fold
+            return (f.train_ids, f.train_counts) if which == 0 else (f.test_ids, f.test_counts)
+        return links_to_arrays(self.links if which == 0 else self.test_links, self.R)
+
+    def _n_links(self, which=0):
+        if self._fold is not None and self._fold_fresh[which]:
+            return int((self._fold.train_ids if which == 0 else self._fold.test_ids).shape[0])
+        return len(self.links if which == 0 else self.test_links)
+
     def _ensure_engine(self):
         from .engine import EMEngine  # imports torch + the HIP library
         key = (self.K, self.P, self._links_version)
@@ -93,10 +148,8 @@ class Model:
                 self._pull()
                 self._engine.close()
             eng = EMEngine(self.K, self.P, B=1, R=self.R, eps=self.eps, device=self._device)
-            ids, counts = links_to_arrays(self.links, self.R)
-            eng.set_links(_lib.SET_TRAIN, ids, counts)
-            tids, tcounts = links_to_arrays(self.test_links, self.R)
-            eng.set_links(_lib.SET_TEST, tids, tcounts)
+            eng.set_links(_lib.SET_TRAIN, *self._link_arrays(0))
+            eng.set_links(_lib.SET_TEST, *self._link_arrays(1))
             self._engine = eng
             self._engine_key = key
             self._dev_fresh = False
@@ -209,6 +262,25 @@ class Model:
         self._links_version += 1
 
     def get_traintest(self, trainfile, testfile):
+        # native reader (include/mmsbm_io.h) for the canonical format on a fresh Model; any other
+        # input takes the reference-semantics loop below
+        fold = None
+        if NATIVE_INGEST and not self.gene_id and not self._n_links(0) and not self._n_links(1):
+            from .ingest import parse_fold
+            fold = parse_fold(trainfile, testfile)
+        if fold is not None:
+            self._fold = fold
+            self.id_gene = dict(enumerate(fold.names))
+            self.gene_id = {g: i for i, g in enumerate(fold.names)}
+            self.uniqueg = dict(enumerate(fold.uniqueg.tolist()))
+            self._links = self._nlinks = self._test_links = None
+            self._fold_fresh = [True, True]
+            self.P = fold.P
+            self._links_version += 1
+            n_train = self._n_links(0)
+            print('READ DATA train', n_train, n_train)
+            print('READ DATA test', self._n_links(1))
+            return
         try:
             gid = 0
             with codecs.open(trainfile, encoding='utf-8', mode='r') as fileref:
@@ -298,8 +370,8 @@ class Model:
         return float(eng.predict(np.array([ids], dtype=np.int32))[0, 0])
 
     def calculate_test_set_results(self):
+        tids, _ = self._link_arrays(1)
         keys = list(self.test_links.keys())
-        tids, _ = links_to_arrays(self.test_links, self.R)
         probs = self._push().predict(tids)[0] if keys else []
         self.results = []
         for p, key in zip(probs, keys):
@@ -308,9 +380,12 @@ class Model:
         self.results.reverse()
 
     def calculate_metrics(self):
-        positives = sum(1 for n in self.links.values() if n[1] == 1)
-        positives_fraction = positives / len(self.links)
-        positives_number = int(positives_fraction * len(self.test_links))
+        if self._fold is not None and self._fold_fresh[0]:
+            positives = int((self._fold.train_counts[:, 1] == 1).sum())
+        else:
+            positives = sum(1 for n in self.links.values() if n[1] == 1)
+        positives_fraction = positives / self._n_links(0)
+        positives_number = int(positives_fraction * self._n_links(1))
         cut_value = 0
         if positives_number < len(self.results):
             cut_value = self.results[positives_number][0]
@@ -343,7 +418,7 @@ class Model:
         text = "Max Likelihood:\t" + str(self.likelihood) + "\n"
         text += "Held-out Likelihood:\t" + str(self.compute_likelihood('test')) + "\n"
         text += "Number of genes (P):\t" + str(self.P) + "\n"
-        text += "Number of links:\t" + str(len(self.links)) + "\n"
+        text += "Number of links:\t" + str(self._n_links(0)) + "\n"
         text += "Number of groups of genes (K):\n" + str(self.K) + "\n"
         text += "Number of possible ratings (R):\n" + str(self.R) + "\n\n"
         self.calculate_test_set_results()
