@@ -949,10 +949,18 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Optional per-wave phase clock (MMSBM_TRACE, measurement only): [wave][16] cycle sums.
+// Optional per-wave phase clock (measurement builds only: -DEMX_TRACE=1, then MMSBM_TRACE=1):
+// [wave][16] cycle sums.  Compiled out of the product build: each clock read would split the
+// loop body into separate basic blocks and keep the scheduler from moving loads across them.
+#ifndef EMX_TRACE
+#define EMX_TRACE 0
+#endif
 struct XTrace {
   unsigned long long* out;
-  __device__ __forceinline__ unsigned long long now() const { return out ? clock64() : 0ull; }
+  __device__ __forceinline__ unsigned long long now() const {
+    if constexpr (EMX_TRACE) return out ? clock64() : 0ull;
+    return 0ull;
+  }
 };
 
 template <int K>
@@ -1221,7 +1229,7 @@ __global__ __launch_bounds__(XPlan<K>::NT) void emx_kernel(
     const int g = 4 * (t % NG) + (ln & 3);
     if (cell < K2 && g < K) rowS[cell * K + g] = s;
   }
-  if (tr.out && lane == 0) {
+  if (EMX_TRACE && tr.out && lane == 0) {
     const unsigned long long t_end = tr.now();
     unsigned long long* o = tr.out + ((size_t)(b * gridDim.x + w) * NW + wv) * 16;
     for (int q = 0; q < 6; ++q) o[q] = tph[q];
@@ -2086,7 +2094,7 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   c->device = device;
   if (const char* ab = getenv("MMSBM_ABLATE")) c->ablate = atoi(ab);
   if (const char* v = getenv("MMSBM_ESTEP")) c->estep_variant = atoi(v);
-  if (getenv("MMSBM_TRACE")) {
+  if (EMX_TRACE && getenv("MMSBM_TRACE")) {
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipMalloc(&c->trace, sizeof(unsigned long long) * 16 * 65536));
   }
