@@ -204,7 +204,8 @@ def main():
         # roofline of the dominant kernel (the E-step), per launch; SURVEY.md §8d figures.
         # Fused path (FP64 MFMA): the E-step launch does Y, Z, W and S = 8 K^3 per observation;
         # VALU path: the E-step does Y, Z, W = 6 K^3 (S is M1's 2 K^3).
-        fused = eng.fused
+        fused = eng.fused                 # E-step + S in one launch (K <= 12)
+        kind = eng.fused_kind             # 0 VALU, 1/2 fused MFMA, 3 large-K MFMA E-step
         est_avg_s = est_b2b_ms / 1e3
         flops = (8.0 if fused else 6.0) * K ** 3 * E_obs * B
         hbm_bytes = (16.0 * E_obs + 16.0 * host.P * K + 24.0 * K ** 3 * 2) * B
@@ -237,12 +238,13 @@ def main():
                        "parallelism": ("link-sharded x%d" if links_mode else "restart-sharded x%d") % world},
             "final_loglik": float(L_all[0]),
             "final_loglik_best": float(L_all.max()),
-            "roofline": {"bound": "mfma" if fused else "fp64-valu", "achieved": achieved_tf,
+            "roofline": {"bound": "mfma" if kind else "fp64-valu", "achieved": achieved_tf,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "kernel": {1: "emx_kernel<%d> (E-step + S, FP64 MFMA)",
-                                    2: "eml_kernel<%d> (E-step + S, FP64 MFMA, lean)"}.get(
-                                        eng.fused_kind, "estep_kernel<%d> (VALU)") % K,
+                                    2: "eml_kernel<%d> (E-step + S, FP64 MFMA, lean)",
+                                    3: "emb_kernel<%d> (E-step, FP64 MFMA; S in m1x_kernel)"}.get(
+                                        kind, "estep_kernel<%d> (VALU)") % K,
                          "avg_launch_us": est_avg_s * 1e6,
                          "algorithmic_flops_per_launch": flops,
                          "hbm": {"achieved": hbm_bytes / est_avg_s / 1e9, "peak": HBM_PEAK_GBS,

@@ -153,7 +153,7 @@ def test_estep_variants_agree(tmp_path, monkeypatch):
 @pytest.mark.parametrize("K", [3, 10, 12])
 @pytest.mark.parametrize("groups", ["1", "256"])
 def test_lean_fused_estep_matches_oracle(tmp_path, monkeypatch, K, groups):
-    """MMSBM_ESTEP=5 (fused E-step without the KR image, 3 waves per SIMD) matches the oracle:
+    """MMSBM_ESTEP=5 (fused E-step without the KR image) matches the oracle:
     one workgroup for everything and the default split, ragged last groups, padded lanes."""
     tr, te = _fold(tmp_path, 300, 5000, seed=40 + K, multi_frac=0.05, both_frac=0.02)
     monkeypatch.setenv("MMSBM_ESTEP", "5")
@@ -170,10 +170,11 @@ def test_lean_fused_estep_matches_oracle(tmp_path, monkeypatch, K, groups):
     np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
 
 
-@pytest.mark.parametrize("K,kind", [(2, 1), (10, 1), (11, 2), (12, 2), (13, 0)])
+@pytest.mark.parametrize("K,kind", [(2, 1), (10, 1), (11, 2), (12, 2), (13, 3), (32, 3)])
 def test_default_estep_kernel_choice(tmp_path, K, kind):
     """Default dispatch: KR-image fused kernel up to K=10, lean fused kernel at K=11/12 (the
-    KR-image kernel only fits 4 waves there), VALU path above; each matches the oracle."""
+    KR-image kernel only fits 4 waves there), large-K MFMA E-step + S kernels above; each
+    matches the oracle."""
     tr, te = _fold(tmp_path, 200, 3000, seed=60 + K, multi_frac=0.05)
     m = _gpu_model(tr, te)
     random.seed(K)
@@ -181,6 +182,54 @@ def test_default_estep_kernel_choice(tmp_path, K, kind):
     theta0, pr0 = np.array(m.theta), np.array(m.pr)
     m.make_iterations(2)
     assert m._engine.fused_kind == kind
+    th_o, pr_o, _, _ = _oracle_run(m, theta0, pr0, 2)
+    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("K,P,E,B", [(13, 200, 3000, 1), (17, 150, 2500, 2), (24, 120, 2000, 1),
+                                     (29, 100, 1500, 1), (32, 100, 1200, 2)])
+@pytest.mark.parametrize("groups", ["1", "256"])
+def test_large_k_mfma_path_matches_oracle(tmp_path, monkeypatch, K, P, E, B, groups):
+    """emb_kernel (p_r staged in a-chunks above K ~ 22, lockstep rounds, idle waves in the last
+    round) + m1x_kernel (4 x 4 (a, b) tiles per wave) against the oracle, per sample of a batch;
+    one workgroup for everything and the default split."""
+    from oracle import c_oracle
+    from trigenicinteractionpredictor_amd import EMEngine
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    monkeypatch.setenv("MMSBM_SACC_WGS", groups)
+    tr, te = _fold(tmp_path, P, E, seed=70 + K, multi_frac=0.05, both_frac=0.02)
+    m = _gpu_model(tr, te)
+    random.seed(K)
+    thetas, prs = [], []
+    for _ in range(B):
+        m.initialize_parameters(K)
+        thetas.append(np.array(m.theta))
+        prs.append(np.array(m.pr))
+    eng = EMEngine(K, m.P, B=B)
+    ids, counts = links_to_arrays(m.links)
+    eng.set_links(0, ids, counts)
+    assert eng.fused_kind == 3
+    eng.upload(np.stack(thetas), np.stack(prs))
+    eng.iterate(2)
+    th, pr = eng.download()
+    for b in range(B):
+        th_o, pr_o = thetas[b], prs[b]
+        for _ in range(2):
+            th_o, pr_o = c_oracle.make_iteration(ids, counts, th_o, pr_o)
+        np.testing.assert_allclose(th[b], th_o, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(pr[b], pr_o, rtol=RTOL, atol=ATOL)
+
+
+def test_large_k_valu_variant_still_matches(tmp_path, monkeypatch):
+    monkeypatch.setenv("MMSBM_ESTEP", "1")
+    tr, te = _fold(tmp_path, 150, 2000, seed=5, multi_frac=0.05)
+    m = _gpu_model(tr, te)
+    random.seed(2)
+    m.initialize_parameters(20)
+    theta0, pr0 = np.array(m.theta), np.array(m.pr)
+    m.make_iterations(2)
+    assert m._engine.fused_kind == 0
     th_o, pr_o, _, _ = _oracle_run(m, theta0, pr0, 2)
     np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)

@@ -1480,6 +1480,299 @@ __global__ __launch_bounds__(XLPlan<K>::NT) void eml_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Large-K FP64-MFMA path (13 <= K <= 32): E-step kernel emb_kernel<K>
+// (U, Y, Z, W; c) then S accumulation m1x_kernel<K>, then m2_kernel on the same partial-row
+// layout as the fused path (fused_rows).  Operand layout as in emx_kernel (lane = 16 hi + 4 blk
+// + lo; A[blk][lo][hi], B[blk][hi][lo], D[blk][hi][lo]).
+//
+// emb_kernel: one 16-observation group per wave per round; the workgroup's waves run in
+// lockstep rounds because p_r is staged in LDS in chunks of CH a-values (K^2 K doubles do not
+// fit above K ~ 22): per chunk, every wave accumulates
+//   U[oD][a][b] = sum_g p[a][b][g] th_k[oD][g]        (NG x NG MFMAs per a; A = th_k of oA)
+//   Y[oD][a] = sum_b th_j[b] U[a][b]  (quad butterfly; the lane keeps a = 4 j + lo)
+//   Z[oD][b] += th_i[a] U[a][b]       (b = 4 bb + lo, complete in the lane)
+//   W[oD][g] += sum_b th_i[oA][a] th_j[oA][b] p[a][b][g]   (k = b = 4 bb + hi, NG x NG MFMAs)
+// and after the last chunk d = eps + sum_b th_j[b] Z[b], c = n / d; c Y, c Z, c W go to the
+// observation's three gene-CSR rows and c to cvec (M1 input).  Rounds = ceil(groups / NW); a
+// wave without a group in the last round computes on a repeated group and stores nothing.
+// ------------------------------------------------------------------------------------------
+template <int K>
+struct BPlan {
+  static constexpr int NG = (K + 3) / 4, KP = 4 * NG;
+  static constexpr int K2 = K * K, K3 = K * K * K;
+  static constexpr int NW = 8, NT = 64 * NW;
+  static constexpr int IS = KP + 1;                  // image row stride (odd)
+  static constexpr int IMG = 2 * XG * IS;            // th_i / th_j rows of the wave's group
+  static constexpr int LDS_CAP = 160 * 1024 / 8;     // doubles
+  static constexpr int PAD_ROWS = KP - K + 1;        // b reads past K in the last a of a chunk
+  static constexpr int CH_FIT = (LDS_CAP - NW * IMG - PAD_ROWS * KP) / (K * KP);
+  static constexpr int CH = CH_FIT < K ? CH_FIT : K; // a-values per staged chunk
+  static constexpr int NCH = (K + CH - 1) / CH;
+  static constexpr int PW_DBL = (CH * K + PAD_ROWS) * KP;
+  static constexpr int LDS_BYTES = (PW_DBL + NW * IMG) * 8;
+  static constexpr bool ON = K >= 13 && K <= 32 && CH >= 1;
+  static_assert(!ON || LDS_BYTES <= 160 * 1024, "big-K E-step LDS plan over budget");
+};
+
+template <int K>
+__global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
+    const int4* __restrict__ obs, const int4* __restrict__ pos, const double* __restrict__ theta,
+    const double* __restrict__ pr, double* __restrict__ contrib, double* __restrict__ cvec,
+    SRows rg, int P, int R, long long n_obs_pad, long long nnz, double eps) {
+  using X = BPlan<K>;
+  constexpr int NG = X::NG, KP = X::KP, K3 = X::K3, IS = X::IS, NW = X::NW, NT = X::NT;
+  constexpr int CH = X::CH, NCH = X::NCH;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Pw = smem;  // [CH K + PAD_ROWS][KP]: rows (a - a0) K + b, columns g (zero padded)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* TI = smem + X::PW_DBL + wv * X::IMG;  // [XG][IS]
+  double* TJ = TI + XG * IS;
+  const int hi = lane >> 4, lo = lane & 3;
+  const int oA = lane & 15, oD = 4 * ((lane >> 2) & 3) + hi;
+  const int w = blockIdx.x, b = blockIdx.y;
+  int r = 0;
+  while (r + 1 < R && w >= rg.whi[r]) ++r;  // workgroup-uniform
+  const int nwg = rg.whi[r] - rg.wlo[r], lw = w - rg.wlo[r];
+  const int ng = rg.grp[r + 1] - rg.grp[r];
+  const int g0 = rg.grp[r] + (int)((long long)lw * ng / nwg);
+  const int g1 = rg.grp[r] + (int)((long long)(lw + 1) * ng / nwg);
+  const int rounds = (g1 - g0 + NW - 1) / NW;
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+  const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
+  double* __restrict__ cb = contrib + (size_t)b * (nnz + 1) * K;
+
+  auto stage = [&](int a0) {  // chunk of a-values [a0, a0 + CH) (rows past K^2 are zero)
+    for (int idx = tid; idx < X::PW_DBL; idx += NT) {
+      const int g = idx % KP, row = idx / KP;
+      const int src = a0 * K + row;  // (a, b) cell index
+      Pw[idx] = (g < K && src < K * K) ? p[(size_t)src * K + g] : 0.0;
+    }
+  };
+  if constexpr (NCH == 1) {
+    stage(0);
+    __syncthreads();
+  }
+
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int gq = g0 + rd * NW + wv;
+    const bool active = gq < g1;
+    const size_t r0 = (size_t)(active ? gq : g0) * XG;
+    const int4 eA = obs[r0 + oA], eD = obs[r0 + oD], qD = pos[r0 + oD];
+    double aU[NG], tjD[NG], tjA[NG];
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      const int g = 4 * s + hi, v = 4 * s + lo;
+      aU[s] = g < K ? th[(size_t)eA.z * K + g] : 0.0;
+      tjD[s] = v < K ? th[(size_t)eD.y * K + v] : 0.0;
+      TI[oD * IS + v] = v < K ? th[(size_t)eD.x * K + v] : 0.0;
+      TJ[oD * IS + v] = tjD[s];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < NG; ++s) tjA[s] = TJ[oA * IS + 4 * s + hi];
+
+    double ysel[NG], zp[NG], wacc[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      ysel[j] = 0.0;
+      zp[j] = 0.0;
+      wacc[j] = 0.0;
+    }
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int a0 = ch * CH;
+      const int a1 = a0 + CH < K ? a0 + CH : K;
+      if constexpr (NCH > 1) {
+        __syncthreads();  // every wave is done with the previous chunk
+        stage(a0);
+        __syncthreads();
+      }
+#pragma unroll 1
+      for (int a = a0; a < a1; ++a) {
+        const double* Pa = Pw + (size_t)(a - a0) * K * KP;
+        // U-phase: acc[bb] = U[oD][a][4 bb + lo]
+        double acc[NG];
+#pragma unroll
+        for (int bb = 0; bb < NG; ++bb) acc[bb] = 0.0;
+#pragma unroll
+        for (int s = 0; s < NG; ++s) {
+          double bf[NG];
+#pragma unroll
+          for (int bb = 0; bb < NG; ++bb) bf[bb] = Pa[(4 * bb + lo) * KP + 4 * s + hi];
+#pragma unroll
+          for (int bb = 0; bb < NG; ++bb) acc[bb] = mfma4(aU[s], bf[bb], acc[bb]);
+        }
+        // W-phase: A = th_i[oA][a] th_j[oA][4 bb + hi], B = p[a][4 bb + hi][4 u + lo]
+        const double tia = TI[oA * IS + a];
+#pragma unroll
+        for (int bb = 0; bb < NG; ++bb) {
+          const double av = tia * tjA[bb];
+          const double* pb = Pa + (4 * bb + hi) * KP + lo;
+#pragma unroll
+          for (int u = 0; u < NG; ++u) wacc[u] = mfma4(av, pb[4 * u], wacc[u]);
+        }
+        const double ta = TI[oD * IS + a];
+        double y = 0.0;
+#pragma unroll
+        for (int bb = 0; bb < NG; ++bb) {
+          y = fma(tjD[bb], acc[bb], y);
+          zp[bb] = fma(ta, acc[bb], zp[bb]);
+        }
+        y += quad_perm<0xB1>(y);
+        y += quad_perm<0x4E>(y);
+#pragma unroll
+        for (int j = 0; j < NG; ++j)
+          if (a == 4 * j + lo) ysel[j] = y;
+      }
+    }
+    double dsum = 0.0;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) dsum = fma(tjD[j], zp[j], dsum);
+    dsum += quad_perm<0xB1>(dsum);
+    dsum += quad_perm<0x4E>(dsum);
+    const double c = (double)eD.w / (dsum + eps);
+    if (active) {
+      const bool real = qD.x >= 0;  // padding observations write the trash row (nnz)
+      double* ri = cb + (size_t)(real ? qD.x : nnz) * K;
+      double* rj = cb + (size_t)(real ? qD.y : nnz) * K;
+      double* rk = cb + (size_t)(real ? qD.z : nnz) * K;
+      double* trash = cb + (size_t)nnz * K;
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        const int v = 4 * j + lo;
+        const int vs = v < K ? v : K - 1;
+        (v < K ? ri : trash)[vs] = c * ysel[j];
+        (v < K ? rj : trash)[vs] = c * zp[j];
+        (v < K ? rk : trash)[vs] = c * wacc[j];
+      }
+      if (lo == 0) cvec[(size_t)b * n_obs_pad + r0 + oD] = c;  // one writer per observation
+    }
+    wave_lds_sync();  // image reads of this round done before the next round's writes
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// m1x_kernel<K>: S_r[a][b][g] = sum_o c_o th_i[o][a] th_j[o][b] th_k[o][g] on FP64 MFMA, grid
+// (G, B) over the fused_rows workgroup ranges (one rating per workgroup), NW waves.  The
+// workgroup stages SG groups (16 SG observations) at a time: c th_i, th_j, th_k rows in LDS.
+// S is tiled in 4 x 4 (a, b) blocks (ta, tb) x 4 g: block blk of the MFMA takes a = 4 ta + blk,
+// rows b = 4 tb + lo (A) / 4 tb + hi (D), k = 4 observations (o = 4 s + hi), g = 4 u + lo.
+// Wave wv owns the tiles t = ta NG + tb with t % NW == wv: accumulators stay in registers for
+// the whole range and each wave writes its own tiles of the partial row: no cross-wave sum.
+// ------------------------------------------------------------------------------------------
+template <int K>
+struct MXPlan {
+  static constexpr int NG = (K + 3) / 4, KP = 4 * NG, K3 = K * K * K;
+  static constexpr int NW = 8, NT = 64 * NW;
+  static constexpr int NTILE = NG * NG;
+  static constexpr int TPW = (NTILE + NW - 1) / NW;  // tiles per wave (last ones may be empty)
+  static constexpr int IS = KP + 1;
+  static constexpr int SG = 4;                       // groups staged per round
+  static constexpr int OBS = SG * XG;
+  static constexpr int IMG = 3 * OBS * IS;
+  static constexpr int LDS_BYTES = (2 * IMG + 2 * OBS) * 8;
+  static constexpr bool ON = K >= 13 && K <= 32 && LDS_BYTES <= 160 * 1024;
+};
+
+template <int K>
+__global__ __launch_bounds__(MXPlan<K>::NT) void m1x_kernel(
+    const int4* __restrict__ obs, const double* __restrict__ theta, const double* __restrict__ cvec,
+    double* __restrict__ partS, SRows rg, int P, int R, long long n_obs_pad, int G) {
+  using X = MXPlan<K>;
+  constexpr int NG = X::NG, IS = X::IS, NW = X::NW, NT = X::NT, TPW = X::TPW, K3 = X::K3;
+  constexpr int OBS = X::OBS, IMG = X::IMG;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
+  const int w = blockIdx.x, b = blockIdx.y;
+  int r = 0;
+  while (r + 1 < R && w >= rg.whi[r]) ++r;
+  const int nwg = rg.whi[r] - rg.wlo[r], lw = w - rg.wlo[r];
+  const int ng = rg.grp[r + 1] - rg.grp[r];
+  const int g0 = rg.grp[r] + (int)((long long)lw * ng / nwg);
+  const int g1 = rg.grp[r] + (int)((long long)(lw + 1) * ng / nwg);
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+  const double* __restrict__ cv = cvec + (size_t)b * n_obs_pad;
+
+  double acc[TPW][NG];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int u = 0; u < NG; ++u) acc[t][u] = 0.0;
+
+  // staging: thread -> (observation, slot, entry); c th_i in TIc, th_j in TJ, th_k in TK
+  auto stage = [&](double* img, int grp0) {
+    double* TIc = img;
+    double* TJ = img + OBS * IS;
+    double* TK = img + 2 * OBS * IS;
+    for (int idx = tid; idx < 3 * OBS * NG * 4; idx += NT) {
+      const int v = idx % (4 * NG), rest = idx / (4 * NG);
+      const int sl = rest % 3, o = rest / 3;
+      const int grp = grp0 + o / XG;
+      const size_t row = (size_t)grp * XG + o % XG;
+      double val = 0.0;
+      if (grp < g1 && v < K) {
+        const int4 e = obs[row];
+        const int gene = sl == 0 ? e.x : (sl == 1 ? e.y : e.z);
+        val = th[(size_t)gene * K + v];
+        if (sl == 0) val *= cv[row];
+      }
+      (sl == 0 ? TIc : (sl == 1 ? TJ : TK))[o * IS + v] = val;
+    }
+  };
+
+  double* img0 = smem;
+  double* img1 = smem + IMG;
+  int grp = g0;
+  if (grp < g1) stage(img0, grp);
+  __syncthreads();
+  int cur = 0;
+  while (grp < g1) {
+    const int nxt = grp + X::SG;
+    double* img = cur ? img1 : img0;
+    if (nxt < g1) stage(cur ? img0 : img1, nxt);  // next round's rows while this one computes
+    const double* TIc = img;
+    const double* TJ = img + OBS * IS;
+    const double* TK = img + 2 * OBS * IS;
+    const int nobs = (g1 - grp < X::SG ? g1 - grp : X::SG) * XG;
+#pragma unroll 1
+    for (int s = 0; s < nobs / 4; ++s) {
+      const int o = 4 * s + hi;
+      double bk[NG];
+#pragma unroll
+      for (int u = 0; u < NG; ++u) bk[u] = TK[o * IS + 4 * u + lo];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int tile = t * NW + wv;
+        if (tile < X::NTILE) {  // wave-uniform
+          const int ta = tile / NG, tb = tile % NG;
+          const double av = TIc[o * IS + 4 * ta + blk] * TJ[o * IS + 4 * tb + lo];
+#pragma unroll
+          for (int u = 0; u < NG; ++u) acc[t][u] = mfma4(av, bk[u], acc[t][u]);
+        }
+      }
+    }
+    __syncthreads();  // reads of this round and writes of the next round both complete
+    cur ^= 1;
+    grp = nxt;
+  }
+  double* __restrict__ rowS = partS + ((size_t)b * G + w) * K3;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = t * NW + wv;
+    if (tile < X::NTILE) {
+      const int a = 4 * (tile / NG) + blk, bq = 4 * (tile % NG) + hi;
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        const int g = 4 * u + lo;
+        if (a < K && bq < K && g < K) rowS[((size_t)a * K + bq) * K + g] = acc[t][u];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // M2, grid (p_blocks + P, B), block 256.
 //  blocks [0, p_blocks): p (:1021-1028), 8 cells x 32 row slices per block.  Partial row n
 //    (n < NR = G * rs) sits at partS + (b * NR + n) * K3 and belongs to rating n % R (M1
@@ -1755,6 +2048,9 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 struct Launch {
   bool fused;  // emx_kernel compiled for this K
   bool lean;   // eml_kernel is the default fused kernel for this K
+  bool big;    // large-K MFMA path (emb_kernel + m1x_kernel) compiled for this K
+  int (*emb)(mmsbm_ctx*, hipStream_t);
+  int (*m1x)(mmsbm_ctx*, hipStream_t);
   int (*emx)(mmsbm_ctx*, hipStream_t);
   int (*estep)(mmsbm_ctx*, hipStream_t);
   int (*m1)(mmsbm_ctx*, hipStream_t);
@@ -1964,6 +2260,51 @@ int launch_eml(mmsbm_ctx* c, hipStream_t s) {
 }
 
 template <int K>
+int launch_emb(mmsbm_ctx* c, hipStream_t s) {
+  if constexpr (BPlan<K>::ON) {
+    const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
+    if (tr.ntiles == 0) return MMSBM_OK;
+    int G = 1;
+    const SRows rg = fused_rows(c, &G);
+    static bool attr = false;
+    if (!attr) {
+      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&emb_kernel<K>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, BPlan<K>::LDS_BYTES));
+      attr = true;
+    }
+    emb_kernel<K><<<dim3(G, c->B), BPlan<K>::NT, BPlan<K>::LDS_BYTES, s>>>(
+        tr.obs, reinterpret_cast<const int4*>(c->pos), c->theta_mut, c->pr_mut, c->contrib,
+        c->cvec, rg, c->P, c->R, tr.n_obs_pad, c->nnz, c->eps);
+    HIP_TRY(hipGetLastError());
+    return MMSBM_OK;
+  } else {
+    return fail(MMSBM_ERR_UNSUPPORTED, "large-K MFMA E-step not compiled for K=%d", K);
+  }
+}
+
+template <int K>
+int launch_m1x(mmsbm_ctx* c, hipStream_t s) {
+  if constexpr (MXPlan<K>::ON) {
+    const LinkSet& tr = c->sets[MMSBM_SET_TRAIN];
+    if (tr.ntiles == 0) return MMSBM_OK;
+    int G = 1;
+    const SRows rg = fused_rows(c, &G);
+    static bool attr = false;
+    if (!attr) {
+      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&m1x_kernel<K>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, MXPlan<K>::LDS_BYTES));
+      attr = true;
+    }
+    m1x_kernel<K><<<dim3(G, c->B), MXPlan<K>::NT, MXPlan<K>::LDS_BYTES, s>>>(
+        tr.obs, c->theta_mut, c->cvec, c->partS, rg, c->P, c->R, tr.n_obs_pad, G);
+    HIP_TRY(hipGetLastError());
+    return MMSBM_OK;
+  } else {
+    return fail(MMSBM_ERR_UNSUPPORTED, "large-K MFMA S accumulation not compiled for K=%d", K);
+  }
+}
+
+template <int K>
 int launch_emx(mmsbm_ctx* c, hipStream_t s) {
   if constexpr (XLPlan<K>::ON) {
     if (use_lean<K>(c->estep_variant)) return launch_eml<K>(c, s);
@@ -2050,11 +2391,32 @@ int launch_predict(mmsbm_ctx* c, const int* ids, long long n, const double* thet
 template <int... Ks>
 constexpr auto make_table(std::integer_sequence<int, Ks...>) {
   return std::array<Launch, sizeof...(Ks)>{
-      Launch{XPlan<Ks + 1>::ON, lean_default<Ks + 1>(), &launch_emx<Ks + 1>, &launch_estep<Ks + 1>, &launch_m1<Ks + 1>,
+      Launch{XPlan<Ks + 1>::ON, lean_default<Ks + 1>(), BPlan<Ks + 1>::ON && MXPlan<Ks + 1>::ON,
+             &launch_emb<Ks + 1>, &launch_m1x<Ks + 1>, &launch_emx<Ks + 1>, &launch_estep<Ks + 1>, &launch_m1<Ks + 1>,
              &launch_m2<Ks + 1>, &launch_mapply<Ks + 1>, &launch_loglik<Ks + 1>, &launch_predict<Ks + 1>}...};
 }
 
 const auto kTable = make_table(std::make_integer_sequence<int, MMSBM_MAX_K>{});
+
+// Which E-step path mmsbm_iterate runs (MMSBM_ESTEP: 0 default, 1/2 VALU, 5 lean fused):
+//   FUSED  E-step + S in one kernel (emx / eml, K <= 12), then M2
+//   BIG    emb_kernel (E) + m1x_kernel (S) on FP64 MFMA (13 <= K <= 32), then M2
+//   VALU   estep_kernel + m1_kernel, then M2
+enum class EPath { VALU, FUSED, BIG };
+EPath epath(const mmsbm_ctx* c) {
+  const Launch& L = kTable[c->K - 1];
+  if (L.fused && (c->estep_variant == 0 || c->estep_variant == 5)) return EPath::FUSED;
+  if (L.big && c->estep_variant == 0) return EPath::BIG;
+  return EPath::VALU;
+}
+int run_estep(mmsbm_ctx* c, EPath path, hipStream_t s) {
+  const Launch& L = kTable[c->K - 1];
+  return path == EPath::FUSED ? L.emx(c, s) : path == EPath::BIG ? L.emb(c, s) : L.estep(c, s);
+}
+int run_m1(mmsbm_ctx* c, EPath path, hipStream_t s) {
+  const Launch& L = kTable[c->K - 1];
+  return path == EPath::FUSED ? MMSBM_OK : path == EPath::BIG ? L.m1x(c, s) : L.m1(c, s);
+}
 
 int check_shape(const mmsbm_ctx* c) {
   if (c->K < 1 || c->K > MMSBM_MAX_K)
@@ -2254,19 +2616,21 @@ int mmsbm_iterate(mmsbm_ctx* c, double* theta, double* pr, int32_t n_iters, void
   const Launch& L = kTable[c->K - 1];
   c->theta_mut = theta;
   c->pr_mut = pr;
-  const bool fused = L.fused && (c->estep_variant == 0 || c->estep_variant == 5);
+  const EPath path = epath(c);
+  const bool fused = path == EPath::FUSED;
+  const bool fused_rows_layout = path != EPath::VALU;  // partial S rows per fused_rows workgroup
   for (int it = 0; it < n_iters; ++it) {
     const bool mark = c->timing && (it % c->timing_stride == 0);
     if (mark && (rc = timing_mark(c, 0, s))) return rc;
-    if ((rc = fused ? L.emx(c, s) : L.estep(c, s))) return rc;
+    if ((rc = run_estep(c, path, s))) return rc;
     if (mark && (rc = timing_mark(c, 0, s))) return rc;
     if (!fused) {
       if (mark && (rc = timing_mark(c, 1, s))) return rc;
-      if ((rc = L.m1(c, s))) return rc;
+      if ((rc = run_m1(c, path, s))) return rc;
       if (mark && (rc = timing_mark(c, 1, s))) return rc;
     }
     if (mark && (rc = timing_mark(c, 2, s))) return rc;
-    if ((rc = L.m2(c, s, fused))) return rc;
+    if ((rc = L.m2(c, s, fused_rows_layout))) return rc;
     if (mark && (rc = timing_mark(c, 2, s))) return rc;
   }
   if (c->trace && fused && n_iters > 0) {  // measurement only: phase cycles of the last launch
@@ -2304,12 +2668,12 @@ int mmsbm_accumulate(mmsbm_ctx* c, const double* theta, const double* pr, double
   // the E-step kernels only read theta / pr; m2 in sums-out mode writes nth / S, not them
   c->theta_mut = const_cast<double*>(theta);
   c->pr_mut = const_cast<double*>(pr);
-  const bool fused = L.fused && (c->estep_variant == 0 || c->estep_variant == 5);
-  if ((rc = fused ? L.emx(c, s) : L.estep(c, s))) return rc;
-  if (!fused && (rc = L.m1(c, s))) return rc;
+  const EPath path = epath(c);
+  if ((rc = run_estep(c, path, s))) return rc;
+  if ((rc = run_m1(c, path, s))) return rc;
   c->nth_out = nth;
   c->S_out = S;
-  rc = L.m2(c, s, fused);
+  rc = L.m2(c, s, path != EPath::VALU);
   c->nth_out = nullptr;
   c->S_out = nullptr;
   return rc;
@@ -2366,8 +2730,8 @@ int mmsbm_fused(const mmsbm_ctx* c, int32_t* fused) {
   int rc = check_shape(c);
   if (rc) return rc;
   const Launch& L = kTable[c->K - 1];
-  const bool on = L.fused && (c->estep_variant == 0 || c->estep_variant == 5);
-  *fused = !on ? 0 : (c->estep_variant == 5 || L.lean) ? 2 : 1;
+  const EPath path = epath(c);
+  *fused = path == EPath::BIG ? 3 : path == EPath::VALU ? 0 : (c->estep_variant == 5 || L.lean) ? 2 : 1;
   return MMSBM_OK;
 }
 
@@ -2388,14 +2752,14 @@ int mmsbm_time_estep(mmsbm_ctx* c, double* theta, double* pr, int32_t n, void* s
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   const Launch& L = kTable[c->K - 1];
-  const bool fused = L.fused && (c->estep_variant == 0 || c->estep_variant == 5);
+  const EPath path = epath(c);
   c->theta_mut = theta;
   c->pr_mut = pr;
   hipEvent_t e0, e1;
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
   HIP_TRY(hipEventRecord(e0, s));
-  for (int i = 0; i < n && rc == MMSBM_OK; ++i) rc = fused ? L.emx(c, s) : L.estep(c, s);
+  for (int i = 0; i < n && rc == MMSBM_OK; ++i) rc = run_estep(c, path, s);
   HIP_TRY(hipEventRecord(e1, s));
   HIP_TRY(hipEventSynchronize(e1));
   float ms = 0.f;

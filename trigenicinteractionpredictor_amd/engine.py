@@ -145,11 +145,12 @@ class EMEngine:
     @property
     def fused(self) -> bool:
         """True when iterate() runs the fused FP64-MFMA E-step (E-step + S in one kernel)."""
-        return self.fused_kind != 0
+        return self.fused_kind in (1, 2)
 
     @property
     def fused_kind(self) -> int:
-        """0 VALU E-step + M1, 1 fused KR-image kernel (emx), 2 fused lean kernel (eml)."""
+        """0 VALU E-step + M1, 1 fused KR-image kernel (emx), 2 fused lean kernel (eml),
+        3 large-K MFMA E-step (emb) + MFMA S accumulation (m1x)."""
         v = ctypes.c_int32()
         _lib.check(self.lib.mmsbm_fused(self.ctx, ctypes.byref(v)))
         return int(v.value)
