@@ -1654,7 +1654,11 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
 // ------------------------------------------------------------------------------------------
 // m1x_kernel<K>: S_r[a][b][g] = sum_o c_o th_i[o][a] th_j[o][b] th_k[o][g] on FP64 MFMA, grid
 // (G, B) over the fused_rows workgroup ranges (one rating per workgroup), NW waves.  The
-// workgroup stages SG groups (16 SG observations) at a time: c th_i, th_j, th_k rows in LDS.
+// workgroup works in rounds of SG groups (OBS = 16 SG observations): c th_i, th_j, th_k rows
+// of the round in an LDS image (double buffered).  Staging is register-prefetched: thread
+// (o = tid / 8, q = tid % 8) holds the observation record two rounds ahead and its theta
+// entries v = q + 8 m one round ahead, so the gathers' latency hides under the MFMA work and
+// each round costs one workgroup barrier.
 // S is tiled in 4 x 4 (a, b) blocks (ta, tb) x 4 g: block blk of the MFMA takes a = 4 ta + blk,
 // rows b = 4 tb + lo (A) / 4 tb + hi (D), k = 4 observations (o = 4 s + hi), g = 4 u + lo.
 // Wave wv owns the tiles t = ta NG + tb with t % NW == wv: accumulators stay in registers for
@@ -1667,10 +1671,13 @@ struct MXPlan {
   static constexpr int NTILE = NG * NG;
   static constexpr int TPW = (NTILE + NW - 1) / NW;  // tiles per wave (last ones may be empty)
   static constexpr int IS = KP + 1;
-  static constexpr int SG = 4;                       // groups staged per round
-  static constexpr int OBS = SG * XG;
+  static constexpr int SG = 4;                       // groups per round
+  static constexpr int OBS = SG * XG;                // observations per round
+  static constexpr int TPO = NT / OBS;               // staging threads per observation
+  static constexpr int NV = (KP + TPO - 1) / TPO;    // theta entries per thread and slot
   static constexpr int IMG = 3 * OBS * IS;
-  static constexpr int LDS_BYTES = (2 * IMG + 2 * OBS) * 8;
+  static constexpr int LDS_BYTES = 2 * IMG * 8;
+  static_assert(NT % OBS == 0, "staging map needs whole observations per thread set");
   static constexpr bool ON = K >= 13 && K <= 32 && LDS_BYTES <= 160 * 1024;
 };
 
@@ -1679,8 +1686,8 @@ __global__ __launch_bounds__(MXPlan<K>::NT) void m1x_kernel(
     const int4* __restrict__ obs, const double* __restrict__ theta, const double* __restrict__ cvec,
     double* __restrict__ partS, SRows rg, int P, int R, long long n_obs_pad, int G) {
   using X = MXPlan<K>;
-  constexpr int NG = X::NG, IS = X::IS, NW = X::NW, NT = X::NT, TPW = X::TPW, K3 = X::K3;
-  constexpr int OBS = X::OBS, IMG = X::IMG;
+  constexpr int NG = X::NG, KP = X::KP, IS = X::IS, NW = X::NW, NT = X::NT, TPW = X::TPW;
+  constexpr int K3 = X::K3, OBS = X::OBS, IMG = X::IMG, TPO = X::TPO, NV = X::NV, SG = X::SG;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1694,6 +1701,7 @@ __global__ __launch_bounds__(MXPlan<K>::NT) void m1x_kernel(
   const int g1 = rg.grp[r] + (int)((long long)(lw + 1) * ng / nwg);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ cv = cvec + (size_t)b * n_obs_pad;
+  const int nrounds = (g1 - g0 + SG - 1) / SG;
 
   double acc[TPW][NG];
 #pragma unroll
@@ -1701,41 +1709,64 @@ __global__ __launch_bounds__(MXPlan<K>::NT) void m1x_kernel(
 #pragma unroll
     for (int u = 0; u < NG; ++u) acc[t][u] = 0.0;
 
-  // staging: thread -> (observation, slot, entry); c th_i in TIc, th_j in TJ, th_k in TK
-  auto stage = [&](double* img, int grp0) {
-    double* TIc = img;
-    double* TJ = img + OBS * IS;
-    double* TK = img + 2 * OBS * IS;
-    for (int idx = tid; idx < 3 * OBS * NG * 4; idx += NT) {
-      const int v = idx % (4 * NG), rest = idx / (4 * NG);
-      const int sl = rest % 3, o = rest / 3;
-      const int grp = grp0 + o / XG;
-      const size_t row = (size_t)grp * XG + o % XG;
-      double val = 0.0;
-      if (grp < g1 && v < K) {
-        const int4 e = obs[row];
-        const int gene = sl == 0 ? e.x : (sl == 1 ? e.y : e.z);
-        val = th[(size_t)gene * K + v];
-        if (sl == 0) val *= cv[row];
+  // staging role: observation so of a round, entries v = sq + TPO m of each slot
+  const int so = tid / TPO, sq = tid % TPO;
+  auto load_rec = [&](int rd, int4& e, double& c) {  // record + c of round rd (zero if absent)
+    const int grp = g0 + rd * SG + so / XG;
+    const bool ok = rd < nrounds && grp < g1;
+    const size_t row = (size_t)(ok ? grp : g0) * XG + so % XG;
+    e = obs[row];
+    c = ok ? cv[row] : 0.0;
+  };
+  auto load_vals = [&](const int4& e, double c, double (&v)[3][NV]) {
+#pragma unroll
+    for (int m = 0; m < NV; ++m) {
+      const int q = sq + TPO * m;
+      const bool in = q < K;
+      const int qs = in ? q : 0;
+      v[0][m] = in ? c * th[(size_t)e.x * K + qs] : 0.0;
+      v[1][m] = in ? th[(size_t)e.y * K + qs] : 0.0;
+      v[2][m] = in ? th[(size_t)e.z * K + qs] : 0.0;
+    }
+  };
+  auto store_vals = [&](double* img, const double (&v)[3][NV]) {
+#pragma unroll
+    for (int m = 0; m < NV; ++m) {
+      const int q = sq + TPO * m;
+      if (q < KP) {
+#pragma unroll
+        for (int sl = 0; sl < 3; ++sl) img[sl * OBS * IS + so * IS + q] = v[sl][m];
       }
-      (sl == 0 ? TIc : (sl == 1 ? TJ : TK))[o * IS + v] = val;
     }
   };
 
-  double* img0 = smem;
-  double* img1 = smem + IMG;
-  int grp = g0;
-  if (grp < g1) stage(img0, grp);
+  double vals[3][NV];
+  int4 e1;
+  double c1;
+  if (nrounds > 0) {
+    int4 e0;
+    double c0;
+    load_rec(0, e0, c0);
+    load_rec(1, e1, c1);
+    load_vals(e0, c0, vals);
+    store_vals(smem, vals);
+  }
   __syncthreads();
-  int cur = 0;
-  while (grp < g1) {
-    const int nxt = grp + X::SG;
-    double* img = cur ? img1 : img0;
-    if (nxt < g1) stage(cur ? img0 : img1, nxt);  // next round's rows while this one computes
+#pragma unroll 1
+  for (int rd = 0; rd < nrounds; ++rd) {
+    const bool more = rd + 1 < nrounds;  // workgroup-uniform
+    int4 e2;
+    double c2;
+    if (more) {
+      load_vals(e1, c1, vals);  // next round's theta entries (in flight during the MFMAs)
+      load_rec(rd + 2, e2, c2);
+    }
+    const double* img = smem + (rd & 1) * IMG;
     const double* TIc = img;
     const double* TJ = img + OBS * IS;
     const double* TK = img + 2 * OBS * IS;
-    const int nobs = (g1 - grp < X::SG ? g1 - grp : X::SG) * XG;
+    const int nrem = g1 - (g0 + rd * SG);
+    const int nobs = (nrem < SG ? nrem : SG) * XG;
 #pragma unroll 1
     for (int s = 0; s < nobs / 4; ++s) {
       const int o = 4 * s + hi;
@@ -1753,9 +1784,12 @@ __global__ __launch_bounds__(MXPlan<K>::NT) void m1x_kernel(
         }
       }
     }
-    __syncthreads();  // reads of this round and writes of the next round both complete
-    cur ^= 1;
-    grp = nxt;
+    if (more) {
+      store_vals(smem + ((rd + 1) & 1) * IMG, vals);  // buffer last read in round rd - 1
+      e1 = e2;
+      c1 = c2;
+    }
+    __syncthreads();
   }
   double* __restrict__ rowS = partS + ((size_t)b * G + w) * K3;
 #pragma unroll
