@@ -1503,12 +1503,16 @@ struct BPlan {
   static constexpr int NW = 8, NT = 64 * NW;
   static constexpr int IS = KP + 1;                  // image row stride (odd)
   static constexpr int IMG = 2 * XG * IS;            // th_i / th_j rows of the wave's group
+  // p image row stride: PS = 4 (mod 8) doubles makes both fragment reads conflict-free
+  // (U-phase rows 4 bb + lo, columns 4 s + hi; W-phase rows 4 bb + hi, columns 4 u + lo: the
+  // 8 addresses of a 32-lane ds_read_b64 group land on 8 distinct bank pairs)
+  static constexpr int PS = (KP % 8 == 4) ? KP : KP + 4;
   static constexpr int LDS_CAP = 160 * 1024 / 8;     // doubles
   static constexpr int PAD_ROWS = KP - K + 1;        // b reads past K in the last a of a chunk
-  static constexpr int CH_FIT = (LDS_CAP - NW * IMG - PAD_ROWS * KP) / (K * KP);
+  static constexpr int CH_FIT = (LDS_CAP - NW * IMG - PAD_ROWS * PS) / (K * PS);
   static constexpr int CH = CH_FIT < K ? CH_FIT : K; // a-values per staged chunk
   static constexpr int NCH = (K + CH - 1) / CH;
-  static constexpr int PW_DBL = (CH * K + PAD_ROWS) * KP;
+  static constexpr int PW_DBL = (CH * K + PAD_ROWS) * PS;
   static constexpr int LDS_BYTES = (PW_DBL + NW * IMG) * 8;
   static constexpr bool ON = K >= 13 && K <= 32 && CH >= 1;
   static_assert(!ON || LDS_BYTES <= 160 * 1024, "big-K E-step LDS plan over budget");
@@ -1521,9 +1525,9 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
     SRows rg, int P, int R, long long n_obs_pad, long long nnz, double eps) {
   using X = BPlan<K>;
   constexpr int NG = X::NG, KP = X::KP, K3 = X::K3, IS = X::IS, NW = X::NW, NT = X::NT;
-  constexpr int CH = X::CH, NCH = X::NCH;
+  constexpr int CH = X::CH, NCH = X::NCH, PS = X::PS;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* Pw = smem;  // [CH K + PAD_ROWS][KP]: rows (a - a0) K + b, columns g (zero padded)
+  double* Pw = smem;  // [CH K + PAD_ROWS][PS]: rows (a - a0) K + b, columns g (zero padded)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* TI = smem + X::PW_DBL + wv * X::IMG;  // [XG][IS]
@@ -1544,7 +1548,7 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
 
   auto stage = [&](int a0) {  // chunk of a-values [a0, a0 + CH) (rows past K^2 are zero)
     for (int idx = tid; idx < X::PW_DBL; idx += NT) {
-      const int g = idx % KP, row = idx / KP;
+      const int g = idx % PS, row = idx / PS;
       const int src = a0 * K + row;  // (a, b) cell index
       Pw[idx] = (g < K && src < K * K) ? p[(size_t)src * K + g] : 0.0;
     }
@@ -1589,7 +1593,7 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
       }
 #pragma unroll 1
       for (int a = a0; a < a1; ++a) {
-        const double* Pa = Pw + (size_t)(a - a0) * K * KP;
+        const double* Pa = Pw + (size_t)(a - a0) * K * PS;
         // U-phase: acc[bb] = U[oD][a][4 bb + lo]
         double acc[NG];
 #pragma unroll
@@ -1598,7 +1602,7 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
         for (int s = 0; s < NG; ++s) {
           double bf[NG];
 #pragma unroll
-          for (int bb = 0; bb < NG; ++bb) bf[bb] = Pa[(4 * bb + lo) * KP + 4 * s + hi];
+          for (int bb = 0; bb < NG; ++bb) bf[bb] = Pa[(4 * bb + lo) * PS + 4 * s + hi];
 #pragma unroll
           for (int bb = 0; bb < NG; ++bb) acc[bb] = mfma4(aU[s], bf[bb], acc[bb]);
         }
@@ -1607,7 +1611,7 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
 #pragma unroll
         for (int bb = 0; bb < NG; ++bb) {
           const double av = tia * tjA[bb];
-          const double* pb = Pa + (4 * bb + hi) * KP + lo;
+          const double* pb = Pa + (4 * bb + hi) * PS + lo;
 #pragma unroll
           for (int u = 0; u < NG; ++u) wacc[u] = mfma4(av, pb[4 * u], wacc[u]);
         }
@@ -1670,7 +1674,7 @@ struct MXPlan {
   static constexpr int NW = 8, NT = 64 * NW;
   static constexpr int NTILE = NG * NG;
   static constexpr int TPW = (NTILE + NW - 1) / NW;  // tiles per wave (last ones may be empty)
-  static constexpr int IS = KP + 1;
+  static constexpr int IS = (KP % 8 == 4) ? KP : KP + 4;  // = 4 (mod 8): conflict-free fragments
   static constexpr int SG = 4;                       // groups per round
   static constexpr int OBS = SG * XG;                // observations per round
   static constexpr int TPO = NT / OBS;               // staging threads per observation
