@@ -41,6 +41,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -1668,6 +1669,9 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
 // Wave wv owns the tiles t = ta NG + tb with t % NW == wv: accumulators stay in registers for
 // the whole range and each wave writes its own tiles of the partial row: no cross-wave sum.
 // ------------------------------------------------------------------------------------------
+#ifndef MX_OCC4  // measurement builds: -DMX_OCC4=0 keeps m1x_kernel at 2 waves per SIMD
+#define MX_OCC4 1
+#endif
 template <int K>
 struct MXPlan {
   static constexpr int NG = (K + 3) / 4, KP = 4 * NG, K3 = K * K * K;
@@ -1681,12 +1685,14 @@ struct MXPlan {
   static constexpr int NV = (KP + TPO - 1) / TPO;    // theta entries per thread and slot
   static constexpr int IMG = 3 * OBS * IS;
   static constexpr int LDS_BYTES = 2 * IMG * 8;
+  // waves per SIMD (__launch_bounds__ minimum): two workgroups per CU where their LDS fits (K <= 20)
+  static constexpr int OCC = MX_OCC4 && 2 * LDS_BYTES <= 160 * 1024 ? 4 : 2;
   static_assert(NT % OBS == 0, "staging map needs whole observations per thread set");
   static constexpr bool ON = K >= 13 && K <= 32 && LDS_BYTES <= 160 * 1024;
 };
 
 template <int K>
-__global__ __launch_bounds__(MXPlan<K>::NT) void m1x_kernel(
+__global__ __launch_bounds__(MXPlan<K>::NT, MXPlan<K>::OCC) void m1x_kernel(
     const int4* __restrict__ obs, const double* __restrict__ theta, const double* __restrict__ cvec,
     double* __restrict__ partS, SRows rg, int P, int R, long long n_obs_pad, int G) {
   using X = MXPlan<K>;
@@ -1771,23 +1777,31 @@ __global__ __launch_bounds__(MXPlan<K>::NT) void m1x_kernel(
     const double* TK = img + 2 * OBS * IS;
     const int nrem = g1 - (g0 + rd * SG);
     const int nobs = (nrem < SG ? nrem : SG) * XG;
+    // the step loop for a compile-time tile count (no per-tile branch, so the step's LDS
+    // reads are issued together and waited on once)
+    auto steps = [&](auto ntc) {
+      constexpr int NTL = decltype(ntc)::value;
 #pragma unroll 1
-    for (int s = 0; s < nobs / 4; ++s) {
-      const int o = 4 * s + hi;
-      double bk[NG];
+      for (int s = 0; s < nobs / 4; ++s) {
+        const int o = 4 * s + hi;
+        double bk[NG];
 #pragma unroll
-      for (int u = 0; u < NG; ++u) bk[u] = TK[o * IS + 4 * u + lo];
+        for (int u = 0; u < NG; ++u) bk[u] = TK[o * IS + 4 * u + lo];
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        const int tile = t * NW + wv;
-        if (tile < X::NTILE) {  // wave-uniform
+        for (int t = 0; t < NTL; ++t) {
+          const int tile = t * NW + wv;
           const int ta = tile / NG, tb = tile % NG;
           const double av = TIc[o * IS + 4 * ta + blk] * TJ[o * IS + 4 * tb + lo];
 #pragma unroll
           for (int u = 0; u < NG; ++u) acc[t][u] = mfma4(av, bk[u], acc[t][u]);
         }
       }
-    }
+    };
+    // tiles t < TPW - 1 exist for every wave; the last one only where t NW + wv < NTILE
+    if (X::NTILE % NW == 0 || (TPW - 1) * NW + wv < X::NTILE)
+      steps(std::integral_constant<int, TPW>{});
+    else
+      steps(std::integral_constant<int, TPW - 1>{});
     if (more) {
       store_vals(smem + ((rd + 1) & 1) * IMG, vals);  // buffer last read in round rd - 1
       e1 = e2;
