@@ -13,8 +13,8 @@ scaling); the final log-likelihoods are gathered over RCCL at the end (:1262-127
 Rank 0 prints ONE JSON line.  `roofline` is measured live with HIP events on the launch stream:
 the dominant kernel (the E-step) is launched back to back right after the timed region and
 its average duration divides the algorithmic FLOPs of one launch; `kernel_us` also gives each
-kernel's in-loop time from event pairs around every 8th iteration's launches (those include the
-dependent-launch boundary).  `cpu_baseline` times the
+kernel's in-loop time from event pairs around the warmup iterations' launches (those include the
+dependent-launch boundary; the timed steps run without events).  `cpu_baseline` times the
 pure-Python CPU restatement of the reference path (oracle/, test infrastructure) on a bounded
 sample of the same workload, on this host, rank 0 at N=1 only.
 """
@@ -61,8 +61,8 @@ def parse():
                          "links: ONE batch of samples whose train links are split over the ranks, "
                          "one all-reduce of the accumulators per iteration (strong scaling, "
                          "SURVEY.md 8e secondary)")
-    ap.add_argument("--event-stride", type=int, default=8,
-                    help="time the kernels of every n-th iteration with HIP events")
+    ap.add_argument("--event-stride", type=int, default=1,
+                    help="time the kernels of every n-th warmup iteration with HIP events")
     return ap.parse_args()
 
 
@@ -167,22 +167,25 @@ def main():
         E_obs = int(build_obs(ids, counts).n_obs)
     runner.upload(np.stack(thetas), np.stack(prs))
 
+    # per-kernel in-loop times come from event pairs in the (untimed) warmup iterations: an
+    # event record between two dependent launches costs the loop ~1-2 us, so the timed region
+    # runs without them
+    eng.timing(0 if args.no_events else args.event_stride)
     runner.iterate(args.warmup)
     torch.cuda.synchronize(dev)
+    est_ms, est_n = eng.timing_result("estep")
+    m1_ms, _ = eng.timing_result("m1")
+    m2_ms, _ = eng.timing_result("m2")
+    eng.timing(False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    eng.timing(0 if args.no_events else args.event_stride)
     t0 = time.perf_counter()
     runner.iterate(args.steps)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    est_ms, est_n = eng.timing_result("estep")
-    m1_ms, _ = eng.timing_result("m1")
-    m2_ms, _ = eng.timing_result("m2")
-    eng.timing(False)
     # the dominant kernel alone, back to back on the same stream (per-launch duration for the
     # roofline; the in-loop events above also time the dependent-launch boundary around it)
     est_b2b_ms = eng.time_estep(args.roofline_launches)

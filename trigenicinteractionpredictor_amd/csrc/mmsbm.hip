@@ -1858,6 +1858,13 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
     __shared__ double tred[256];
     const int slot = tid / K, k = tid % K;
     const int q0 = gptr[g], q1 = gptr[g + 1];
+    double* row = theta + (size_t)b * P * K + (size_t)g * K;
+    // the final update's operands load now, beside the row pointers, not after the reduction
+    double th_old = 0.0, dg = 1.0;
+    if (tid < K && !nth_out) {
+      th_old = row[tid];
+      dg = (double)deg[g];
+    }
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     if (slot < NS) {
       const double* __restrict__ src = contrib + (size_t)b * (nnz + 1) * K + k;
@@ -1879,8 +1886,7 @@ __global__ __launch_bounds__(256) void m2_kernel(double* __restrict__ pr, double
       if (nth_out) {  // link-sharded: this rank's sum, applied after the cross-rank reduction
         nth_out[(size_t)b * P * K + (size_t)g * K + tid] = sum;
       } else {
-        double* row = theta + (size_t)b * P * K + (size_t)g * K;
-        row[tid] = row[tid] * sum / (double)deg[g];
+        row[tid] = th_old * sum / dg;
       }
     }
     return;
