@@ -1,0 +1,16 @@
+# GPU tests, then one bench config across measurement builds (product + build/<lib>.so ...).
+# usage: bash tools/gpu_cfg_libs_ab.sh TAG "bench args" lib1 lib2 ...
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=$1; ARGS=$2; shift 2
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+for rep in 1 2; do
+  for v in prod "$@"; do
+    if [ $v = prod ]; then unset MMSBM_LIB; else export MMSBM_LIB=$GRAFT_REPO_ROOT/build/$v.so; fi
+    timeout -k 10 300 python bench.py --no-cpu-baseline $ARGS > $OUT/$v.$rep.json 2> $OUT/$v.$rep.err || { echo "$v failed"; tail -5 $OUT/$v.$rep.err; exit 1; }
+    python -c "import json;d=json.load(open('$OUT/$v.$rep.json'));print('$v', round(d['value'],1), {k: round(x,1) for k,x in d['kernel_us'].items()}, round(d['roofline']['frac'],3), round(d['final_loglik'],6))"
+  done
+done

@@ -1501,7 +1501,12 @@ template <int K>
 struct BPlan {
   static constexpr int NG = (K + 3) / 4, KP = 4 * NG;
   static constexpr int K2 = K * K, K3 = K * K * K;
-  static constexpr int NW = 8, NT = 64 * NW;
+#ifndef EMB_NW_SMALL  // measurement builds: waves per workgroup where all of p_r fits (K <= 20)
+#define EMB_NW_SMALL 12
+#endif
+  // K <= 20: all of p_r plus 12 waves' images fit in LDS (3 waves per SIMD; K=20 x 8 samples:
+  // 599 -> 544 us against 8 waves, 16 waves 670 us); above, 8 waves and p_r staged in chunks
+  static constexpr int NW = K <= 20 ? EMB_NW_SMALL : 8, NT = 64 * NW;
   static constexpr int IS = KP + 1;                  // image row stride (odd)
   static constexpr int IMG = 2 * XG * IS;            // th_i / th_j rows of the wave's group
   // p image row stride: PS = 4 (mod 8) doubles makes both fragment reads conflict-free
@@ -1547,11 +1552,28 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
   double* __restrict__ cb = contrib + (size_t)b * (nnz + 1) * K;
 
-  auto stage = [&](int a0) {  // chunk of a-values [a0, a0 + CH) (rows past K^2 are zero)
-    for (int idx = tid; idx < X::PW_DBL; idx += NT) {
-      const int g = idx % PS, row = idx / PS;
-      const int src = a0 * K + row;  // (a, b) cell index
-      Pw[idx] = (g < K && src < K * K) ? p[(size_t)src * K + g] : 0.0;
+  // chunk of a-values [a0, a0 + CH) (rows past K^2 are zero).  Loads go out in batches of
+  // SB from clamped (always valid) addresses, then the batch is stored: SB loads in flight
+  // per thread instead of one load-store round trip per element
+  auto stage = [&](int a0) {
+    constexpr int NPER = (X::PW_DBL + NT - 1) / NT, SB = 12;
+#pragma unroll
+    for (int j0 = 0; j0 < NPER; j0 += SB) {
+      double v[SB];
+#pragma unroll
+      for (int j = 0; j < SB; ++j) {
+        const int idx = tid + (j0 + j) * NT;
+        const int g = idx % PS, row = idx / PS;
+        const int src = a0 * K + row;  // (a, b) cell index
+        const bool in = g < K && src < K * K;
+        const double x = p[(size_t)(in ? src : 0) * K + (in ? g : 0)];
+        v[j] = in ? x : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < SB; ++j) {
+        const int idx = tid + (j0 + j) * NT;
+        if (j0 + j < NPER && idx < X::PW_DBL) Pw[idx] = v[j];
+      }
     }
   };
   if constexpr (NCH == 1) {
@@ -1584,13 +1606,18 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
       zp[j] = 0.0;
       wacc[j] = 0.0;
     }
-    for (int ch = 0; ch < NCH; ++ch) {
+    for (int ci = 0; ci < NCH; ++ci) {
+      // odd rounds walk the chunks backwards, so a round starts on the chunk the previous
+      // round ended with, which is still staged: NCH - 1 stagings per round instead of NCH
+      const int ch = (rd & 1) ? NCH - 1 - ci : ci;
       const int a0 = ch * CH;
       const int a1 = a0 + CH < K ? a0 + CH : K;
       if constexpr (NCH > 1) {
-        __syncthreads();  // every wave is done with the previous chunk
-        stage(a0);
-        __syncthreads();
+        if (ci > 0 || rd == 0) {  // workgroup-uniform
+          __syncthreads();  // every wave is done with the previous chunk
+          stage(a0);
+          __syncthreads();
+        }
       }
 #pragma unroll 1
       for (int a = a0; a < a1; ++a) {
