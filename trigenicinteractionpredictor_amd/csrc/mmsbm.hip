@@ -1696,6 +1696,9 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
 // Wave wv owns the tiles t = ta NG + tb with t % NW == wv: accumulators stay in registers for
 // the whole range and each wave writes its own tiles of the partial row: no cross-wave sum.
 // ------------------------------------------------------------------------------------------
+#ifndef MX_STEP_UNROLL  // measurement builds: step-loop unroll of m1x_kernel
+#define MX_STEP_UNROLL 1
+#endif
 #ifndef MX_OCC4  // measurement builds: -DMX_OCC4=0 keeps m1x_kernel at 2 waves per SIMD
 #define MX_OCC4 1
 #endif
@@ -1808,7 +1811,7 @@ __global__ __launch_bounds__(MXPlan<K>::NT, MXPlan<K>::OCC) void m1x_kernel(
     // reads are issued together and waited on once)
     auto steps = [&](auto ntc) {
       constexpr int NTL = decltype(ntc)::value;
-#pragma unroll 1
+#pragma unroll MX_STEP_UNROLL
       for (int s = 0; s < nobs / 4; ++s) {
         const int o = 4 * s + hi;
         double bk[NG];
