@@ -116,9 +116,10 @@ int mmsbm_accumulate(mmsbm_ctx *ctx, const double *theta, const double *pr, doub
 int mmsbm_mstep(mmsbm_ctx *ctx, double *theta, double *pr, const double *nth, const double *S,
                 void *stream);
 
-/* *fused != 0 when mmsbm_iterate runs a fused FP64-MFMA E-step (E-step and S accumulation in
- * one kernel, then M2): 1 = the KR-image kernel (K <= 10), 2 = the lean kernel (K = 11, 12, or
- * MMSBM_ESTEP=5); 0 when it runs the VALU E-step + M1 + M2 (MMSBM_ESTEP=1/2, or K > 12). */
+/* Which E-step path mmsbm_iterate runs: 1 = fused FP64-MFMA KR-image kernel (E-step and S
+ * accumulation in one kernel, then M2; K <= 10), 2 = the lean fused kernel (K = 11, 12, or
+ * MMSBM_ESTEP=5), 3 = the large-K FP64-MFMA pair (E-step kernel, S-accumulation kernel, M2;
+ * 13 <= K <= 32), 0 = the VALU E-step + M1 + M2 (MMSBM_ESTEP=1/2). */
 int mmsbm_fused(const mmsbm_ctx *ctx, int32_t *fused);
 
 /* Kernel timing for measurement (bench.py): with stride n > 0, mmsbm_iterate records a HIP
