@@ -1696,6 +1696,9 @@ __global__ __launch_bounds__(BPlan<K>::NT) void emb_kernel(
 // Wave wv owns the tiles t = ta NG + tb with t % NW == wv: accumulators stay in registers for
 // the whole range and each wave writes its own tiles of the partial row: no cross-wave sum.
 // ------------------------------------------------------------------------------------------
+#ifndef MX_BIG_ROUND  // measurement builds: 128-observation single-buffered rounds at K <= 20
+#define MX_BIG_ROUND 0
+#endif
 #ifndef MX_STEP_UNROLL  // measurement builds: step-loop unroll of m1x_kernel
 #define MX_STEP_UNROLL 1
 #endif
@@ -1709,12 +1712,16 @@ struct MXPlan {
   static constexpr int NTILE = NG * NG;
   static constexpr int TPW = (NTILE + NW - 1) / NW;  // tiles per wave (last ones may be empty)
   static constexpr int IS = (KP % 8 == 4) ? KP : KP + 4;  // = 4 (mod 8): conflict-free fragments
-  static constexpr int SG = 4;                       // groups per round
+  // rounds of SG groups; a single image buffer (two barriers per round) where MX_BIG_ROUND
+  // doubles the round at K <= 20 within the same LDS (measurement switch)
+  static constexpr bool ONEBUF = MX_BIG_ROUND && K <= 20;
+  static constexpr int NBUF = ONEBUF ? 1 : 2;
+  static constexpr int SG = ONEBUF ? 8 : 4;          // groups per round
   static constexpr int OBS = SG * XG;                // observations per round
   static constexpr int TPO = NT / OBS;               // staging threads per observation
   static constexpr int NV = (KP + TPO - 1) / TPO;    // theta entries per thread and slot
   static constexpr int IMG = 3 * OBS * IS;
-  static constexpr int LDS_BYTES = 2 * IMG * 8;
+  static constexpr int LDS_BYTES = NBUF * IMG * 8;
   // waves per SIMD (__launch_bounds__ minimum): two workgroups per CU where their LDS fits (K <= 20)
   static constexpr int OCC = MX_OCC4 && 2 * LDS_BYTES <= 160 * 1024 ? 4 : 2;
   static_assert(NT % OBS == 0, "staging map needs whole observations per thread set");
@@ -1801,7 +1808,7 @@ __global__ __launch_bounds__(MXPlan<K>::NT, MXPlan<K>::OCC) void m1x_kernel(
       load_vals(e1, c1, vals);  // next round's theta entries (in flight during the MFMAs)
       load_rec(rd + 2, e2, c2);
     }
-    const double* img = smem + (rd & 1) * IMG;
+    const double* img = smem + (X::NBUF == 2 ? (rd & 1) * IMG : 0);
     const double* TIc = img;
     const double* TJ = img + OBS * IS;
     const double* TK = img + 2 * OBS * IS;
@@ -1832,8 +1839,10 @@ __global__ __launch_bounds__(MXPlan<K>::NT, MXPlan<K>::OCC) void m1x_kernel(
       steps(std::integral_constant<int, TPW>{});
     else
       steps(std::integral_constant<int, TPW - 1>{});
+    if constexpr (X::NBUF == 1) __syncthreads();  // every wave is done with the image
     if (more) {
-      store_vals(smem + ((rd + 1) & 1) * IMG, vals);  // buffer last read in round rd - 1
+      // double buffered: the buffer last read in round rd - 1; single: the one just read
+      store_vals(smem + (X::NBUF == 2 ? ((rd + 1) & 1) * IMG : 0), vals);
       e1 = e2;
       c1 = c2;
     }
