@@ -63,7 +63,45 @@ def parse():
                          "SURVEY.md 8e secondary)")
     ap.add_argument("--event-stride", type=int, default=1,
                     help="time the kernels of every n-th warmup iteration with HIP events")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks and run the end-of-run gather without any GPU work "
+                         "(CPU test of the N-rank launch path, with --backend gloo)")
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="processes for the aggregate CPU baseline (default: the host cores this "
+                         "process may use, at most 16)")
     return ap.parse_args()
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: start N copies of this script, one rank per GPU (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT as torch.distributed.run sets them), BEFORE this
+    process touches any GPU, and return the worst exit code.  Rank 0 prints the JSON line.
+    (The reference scales the same way, one OS process per batch of samples: src/run.sh:36-45.)"""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0:
+                rc = rc or (code if code > 0 else 128 - code)
+                for q in alive:            # a failed rank would leave the others in a barrier
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def make_fold(P, E, rank):
@@ -74,10 +112,11 @@ def make_fold(P, E, rank):
     return tr, te
 
 
-def cpu_baseline(train, test, K, seed, seconds):
-    """Pure-Python restatement of :984-1043 (bit-identical to the reference under CPython).
-    The per-link loop (:987-1012, all of the cost) is timed on the first n links so that the
-    sample takes ~`seconds` and scaled to all links; the M-step (:1016-1043) is timed whole."""
+def _port_rate(train, test, K, seed, seconds, full):
+    """One CPU process: seconds per EM iteration of the pure-Python restatement of :984-1043.
+    full: time whole make_iteration calls (cheap K); else the per-link loop (:987-1012, all of
+    the cost) on the first n links, n sized so the sample takes ~`seconds`, scaled to every
+    link, plus the M-step (:1016-1043) timed whole.  -> (s_per_iter, links_timed, links)."""
     import contextlib
     import io
     from oracle.mmsbm_oracle import OracleModel
@@ -88,6 +127,13 @@ def cpu_baseline(train, test, K, seed, seconds):
     m.initialize_parameters(K)
     items = list(m.links.items())
     E = len(items)
+    if full:
+        n_it = 0
+        t0 = time.perf_counter()
+        while n_it < 1 or time.perf_counter() - t0 < seconds:
+            m.make_iteration()
+            n_it += 1
+        return (time.perf_counter() - t0) / n_it, E, E
     t0 = time.perf_counter()
     m.accumulate(items[:32])
     per_link = (time.perf_counter() - t0) / 32
@@ -97,29 +143,95 @@ def cpu_baseline(train, test, K, seed, seconds):
     t_loop = time.perf_counter() - t0
     full_deg = [0] * m.P
     for key in m.links:
-        for s in key.split("_"):
-            full_deg[int(s)] += 1
+        for x in key.split("_"):
+            full_deg[int(x)] += 1
     nth = [[1.0] * K for _ in range(m.P)]
     npr = [[[[0.5] * m.R for _ in range(K)] for _ in range(K)] for _ in range(K)]
     t0 = time.perf_counter()
     m.finish(nth, npr, full_deg)
     t_fin = time.perf_counter() - t0
-    full_iter_s = t_loop * E / n + t_fin
-    return {"value": 1.0 / full_iter_s, "unit": "EM-iterations/s", "cores": 1, "kind": "port",
-            "sample": "oracle OracleModel.make_iteration (pure-Python restatement of :984-1043), "
-                      "per-link loop timed on %d of %d train links (%.1f s) and scaled x%.2f, "
-                      "M-step timed whole (%.3f s); K=%d, %s %s, 1 process -> %.1f s/iter" % (
-                          n, E, t_loop, E / n, t_fin, K, platform.python_implementation(),
-                          platform.python_version(), full_iter_s)}
+    return t_loop * E / n + t_fin, n, E
+
+
+def _port_worker(a):
+    return _port_rate(*a)
+
+
+def cpu_baseline(train, test, K, seed, seconds, cores):
+    """The reference path's CPU baseline: the oracle's pure-Python restatement,
+    one process per core, each on its own sample (the reference's own scaling model, src/run.sh
+    :12,16).  Single-core rate alone, then `cores` processes at once (aggregate); config 1's K=2
+    rate from whole iterations.  Runs before this process touches the GPU."""
+    import multiprocessing as mp
+    one, n, E = _port_rate(train, test, K, seed, seconds, False)
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(cores) as pool:
+        many = pool.map(_port_worker, [(train, test, K, seed + c, seconds, False) for c in range(cores)])
+    agg = sum(1.0 / r[0] for r in many)
+    k2, _, _ = _port_rate(train, test, 2, seed, min(seconds, 5.0), True)
+    rec = {"value": agg, "unit": "EM-iterations/s", "cores": cores, "kind": "port",
+           "single_core_value": 1.0 / one,
+           "config1_K2_single_core_value": 1.0 / k2,
+           "sample": ("oracle/mmsbm_oracle.py (pure-Python restatement of :984-1043), %s %s. "
+                      "K=%d: the per-link loop timed on %d of %d train links (%.0f s) and scaled "
+                      "x%.2f to the whole set, M-step timed whole: %.1f s/iteration on 1 core; "
+                      "%d processes at once, each its own sample: aggregate %.4f iterations/s. "
+                      "K=2 (config 1): whole iterations, %.2f s each on 1 core"
+                      % (platform.python_implementation(), platform.python_version(), K, n, E,
+                         seconds, E / n, one, cores, agg, k2))}
+    cal = os.path.join(REPO, "profiles", "cpu_calibration.json")
+    if os.path.exists(cal):
+        with open(cal) as f:
+            rec["calibration"] = json.load(f)     # restatement vs the reference's own loop
+    return rec
+
+
+def launch_check(args, world, rank):
+    """The N-rank path without GPU work: every rank takes its block of sample ids, and the
+    end-of-run gather (RCCL all_gather under nccl) collects them on every rank."""
+    import torch
+    import torch.distributed as dist
+    from trigenicinteractionpredictor_amd.restarts import shard_samples
+    if world > 1:
+        dist.init_process_group(args.backend)
+    ids = shard_samples(args.samples * world, world, rank)
+    mine = torch.tensor([[rank, s] for s in ids], dtype=torch.float64)
+    if world > 1:
+        rows = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(rows, mine)
+        rows = torch.cat(rows)
+    else:
+        rows = mine
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world,
+                          "world_size": dist.get_world_size() if world > 1 else 1,
+                          "gathered_rows": int(rows.shape[0]),
+                          "samples": sorted(int(x) for x in rows[:, 1].tolist())}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+        return 2
+    if args.launch_check:
+        launch_check(args, world, rank)
+        return 0
+    train, test = make_fold(args.P, args.E, rank)
+    cpu_rec = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = args.cpu_cores or min(len(os.sched_getaffinity(0)), 16)
+        cpu_rec = cpu_baseline(train, test, args.K, args.seed, args.cpu_baseline_seconds, cores)
+
+    import torch
+    import torch.distributed as dist
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -134,7 +246,6 @@ def main():
     from trigenicinteractionpredictor_amd import EMEngine, Model
     from trigenicinteractionpredictor_amd.layout import links_to_arrays, build_obs
 
-    train, test = make_fold(args.P, args.E, rank)
     import contextlib
     import io
     with contextlib.redirect_stdout(io.StringIO()):
@@ -198,8 +309,10 @@ def main():
         gathered = [torch.empty_like(L) for _ in range(world)]
         dist.all_gather(gathered, L)       # RCCL gather of final likelihoods
         L_all = torch.cat(gathered).cpu().numpy()
+        n_gathered = int(L_all.shape[0])
     else:
         L_all = L.cpu().numpy()
+        n_gathered = int(L_all.shape[0])
 
     if rank == 0:
         iters_total = args.steps * B * (1 if links_mode else world)
@@ -239,6 +352,8 @@ def main():
                        "P": host.P, "E_train": len(host.links), "E_test": len(host.test_links),
                        "E_obs": E_obs, "samples_per_gpu": B,
                        "parallelism": ("link-sharded x%d" if links_mode else "restart-sharded x%d") % world},
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "gathered_samples": n_gathered,
             "final_loglik": float(L_all[0]),
             "final_loglik_best": float(L_all.max()),
             "roofline": {"bound": "mfma" if kind else "fp64-valu", "achieved": achieved_tf,
@@ -256,16 +371,16 @@ def main():
             "kernel_us": {"estep": est_ms * 1e3 / max(est_n, 1), "estep_back_to_back": est_avg_s * 1e6,
                           "m1": m1_ms * 1e3 / max(est_n, 1),
                           "m2": m2_ms * 1e3 / max(est_n, 1)},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu_rec,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(train, test, K, args.seed, args.cpu_baseline_seconds)
-            line["vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
+        if cpu_rec is not None:
+            line["vs_cpu_baseline"] = value / cpu_rec["value"]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

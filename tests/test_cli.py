@@ -106,3 +106,36 @@ def test_invalid_arguments_exit_2(argv):
 def test_help_exits_0():
     rc, _ = _run(["-h"])
     assert rc == 0
+
+
+def test_batch_mode_matches_reference_loop(tmp_path):
+    """--batch 2 on 3 samples (one full batch and a ragged one): same iterations to convergence,
+    same converged set and output names as the sequential reference loop (:1253-1279); the batched
+    engine is the C oracle here (tests/test_gpu_cli.py runs it on the GPU)."""
+    from oracle_engine import OracleEngine
+    from trigenicinteractionpredictor_amd.model import Model
+
+    written = []
+
+    class M(Model):
+        def to_file(self, name_file=None):
+            written.append((name_file, self.likelihood, [list(r) for r in self._theta]))
+
+    out = str(tmp_path) + os.sep
+    lines = []
+    holder = {}
+
+    def factory():
+        holder["m"] = M()
+        return holder["m"]
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        rc = cli.main(["-k", "2", "-i", "40", "-n", "3", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST,
+                       "-o", out, "--seed", "5", "--batch", "2"], model_factory=factory,
+                      out=lines.append,
+                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links))
+    assert rc == 0
+    ref = _reference_loop(2, 5, 3, 40, 3, 4)
+    got = [l for l in lines if l.startswith("Sample ") and "iterations" in l]
+    assert [(int(l.split()[1][:-1]), int(l.split()[2])) for l in got] == [(s, it) for s, it, _ in ref]
+    assert [w[0] for w in written] == [out + "Sample_%d_K2.csv" % s for s, _, c in ref if c]

@@ -32,3 +32,27 @@ def test_cli_on_gpu_matches_reference_loop(tmp_path):
             assert "Held-out Likelihood:\t" in text and "\nMetrics:\n" in text
             like = float(text.split("\n")[0].split("\t")[1])
             assert np.isfinite(like)
+
+
+def test_cli_batch_mode_on_gpu_matches_reference_loop(tmp_path):
+    """`--batch 2` (samples advanced together in one batched engine) against the sequential
+    reference loop on the oracle: same iterations to convergence, same converged set, same file
+    names; each file's header likelihood equals the oracle's at that iteration."""
+    out = str(tmp_path) + os.sep
+    lines = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        rc = cli.main(["-k", "3", "-i", "60", "-n", "3", "-f", "4", "-b", "6", "-t", TRAIN, "-e", TEST,
+                       "-o", out, "--seed", "7", "--batch", "2"], out=lines.append)
+    assert rc == 0
+    ref = _reference_loop(3, 7, 3, 60, 4, 6)
+    got = [l for l in lines if l.startswith("Sample ") and "iterations" in l]
+    assert [(int(l.split()[1][:-1]), int(l.split()[2])) for l in got] == [(s, it) for s, it, _ in ref]
+    for s, _, conv in ref:
+        path = out + "Sample_%d_K3.csv" % s
+        assert os.path.isfile(path) == conv
+        if conv:
+            text = open(path).read()
+            like = float(text.split("\n")[0].split("\t")[1])
+            want = float([l for l in got if l.startswith("Sample %d:" % s)][0].split()[5])
+            np.testing.assert_allclose(like, want, rtol=1e-12)
+            assert "Held-out Likelihood:\t" in text and "\nTest set:\n" in text

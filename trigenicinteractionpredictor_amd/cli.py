@@ -31,9 +31,13 @@ python -m trigenicinteractionpredictor_amd.cli [-h|--help] [-i|--num_iterations=
     [-f|--fcheck=] <likelihood check frequency, 0: never> [-b|--bcheck=] <first check after>
     [-o|--out=] <output path prefix> [-t|--train=] <train file> [-e|--test=] <test file>
     [-k|--k=] <number of groups> [--seed=] <RNG seed, default: the process id>
+    [--batch=] <samples advanced together on the GPU, default 1>
 
 Defaults: iterations {it}, samples {s}, check frequency {f}, train file {t}, K {k}.
 """
+
+
+MAX_K = 32   # MMSBM_MAX_K (include/mmsbm.h): largest K the kernels are compiled for
 
 
 class ArgError(Exception):
@@ -45,7 +49,7 @@ def parse(argv, defaults):
     try:
         opts, _ = getopt.getopt(argv, "hi:n:s:f:b:o:t:e:k:",
                                 ["help", "num_iterations=", "num_samples=", "sample_ini=", "fcheck=",
-                                 "bcheck=", "out=", "train=", "test=", "k=", "seed="])
+                                 "bcheck=", "out=", "train=", "test=", "k=", "seed=", "batch="])
     except getopt.GetoptError:
         print("Argument error. Aborting")
         raise ArgError()
@@ -101,9 +105,18 @@ def parse(argv, defaults):
                 if int(arg) < 1:
                     print("\n\nERROR: Number of groups should be a positive integer number different from 0")
                     raise ArgError()
+                if int(arg) > MAX_K:     # the engine's compiled kernel set (include/mmsbm.h)
+                    print("\n\nERROR: Number of groups K=%d is above the engine's maximum %d"
+                          % (int(arg), MAX_K))
+                    raise ArgError()
                 cfg["k"] = int(arg)
             elif opt == "--seed":
                 cfg["seed"] = int(arg)
+            elif opt == "--batch":
+                if int(arg) < 1:
+                    print("\n\nERROR: batch size should be a positive integer number")
+                    raise ArgError()
+                cfg["batch"] = int(arg)
         except ValueError:
             raise ArgError()
     return cfg
@@ -145,10 +158,50 @@ def run_sample(model, cfg, sample, outfile, out=print):
 
 
 DEFAULTS = {"iterations": 10000, "samples": 100, "sample_ini": 0, "fcheck": 25, "bcheck": 100,
-            "train": "train0.dat", "test": "test0.dat", "out": "", "k": 1, "seed": None}
+            "train": "train0.dat", "test": "test0.dat", "out": "", "k": 1, "seed": None, "batch": 1}
 
 
-def main(argv=None, model_factory=None, out=print):
+def run_batch(model, cfg, samples, out=print, engine_factory=None):
+    """`--batch B`: the pending samples advance B at a time in one batched engine
+    (restarts.run_samples: the reference's per-sample check schedule and convergence rule,
+    :1262-1279, applied to every sample of the batch).  Initial states come from the one RNG
+    stream in sample order, exactly as the sequential loop draws them (:1260); a converged
+    sample's theta / p snapshot is written through `Model.to_file` (:1275) with its converged
+    train likelihood as `likelihood` (:1269).  Returns [(sample, iterations, converged)]."""
+    import numpy as np
+    from .restarts import run_samples
+    K, B = cfg["k"], cfg["batch"]
+    if engine_factory is None:
+        from .engine import EMEngine
+
+        def engine_factory(n):
+            eng = EMEngine(K, model.P, B=n, R=model.R, eps=model.eps)
+            eng.set_links(0, *model._link_arrays(0))
+            eng.set_links(1, *model._link_arrays(1))
+            return eng
+    done = []
+    for lo in range(0, len(samples), B):
+        block = samples[lo:lo + B]
+        thetas, prs = [], []
+        for s in block:                        # draws in sample order, like :1260
+            model.initialize_parameters(K)
+            thetas.append(np.array(model._theta, dtype=np.float64))
+            prs.append(np.array(model._pr, dtype=np.float64))
+        res = run_samples(engine_factory(len(block)), block, thetas, prs, cfg["iterations"],
+                          cfg["fcheck"], cfg["bcheck"], keep_params=True)
+        for r in res:
+            out("Sample " + str(r.sample) + ": " + str(r.iterations) + " iterations, likelihood "
+                + str(r.loglik) + (" (converged)" if r.converged else ""))
+            if r.converged:
+                model.theta = r.theta.tolist()
+                model.pr = r.pr.tolist()
+                model.likelihood = r.loglik
+                model.to_file(cfg["out"] + "Sample_" + str(r.sample) + "_K" + str(K) + ".csv")
+            done.append((r.sample, r.iterations, r.converged))
+    return done
+
+
+def main(argv=None, model_factory=None, out=print, engine_factory=None):
     cfg = dict(DEFAULTS)
     cfg["seed"] = os.getpid()                                    # :1149
     try:
@@ -174,11 +227,17 @@ def main(argv=None, model_factory=None, out=print):
     model = model_factory()
     model.get_traintest(cfg["train"], cfg["test"])
     out("\nStarting algorithm...")
+    pending = []
     for sample in range(cfg["sample_ini"], cfg["sample_ini"] + int(cfg["samples"])):
         outfile = cfg["out"] + "Sample_" + str(sample) + "_K" + str(cfg["k"]) + ".csv"
         if os.path.isfile(outfile):                              # :1256-1257
             continue
-        run_sample(model, cfg, sample, outfile, out)
+        if cfg["batch"] > 1:
+            pending.append(sample)
+        else:
+            run_sample(model, cfg, sample, outfile, out)
+    if pending:
+        run_batch(model, cfg, pending, out, engine_factory)
     return 0
 
 

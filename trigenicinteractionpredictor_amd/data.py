@@ -164,3 +164,17 @@ def _write_fold_numpy(spec: FoldSpec, train_path: str, test_path: str):
     dump(train_path, train)
     dump(test_path, test)
     return int(train.shape[0]), int(test.shape[0])
+
+
+def synthetic_links(spec: FoldSpec):
+    """Train link table of a synthetic fold as arrays, without writing files (the 10M-link
+    stress configuration): ids int32[E_train][3] (each triple sorted ascending), counts
+    int32[E_train][2] with one observation per link, rating Bernoulli(``pos_frac``)."""
+    cover, rest, rs = _numpy_triples(spec)
+    n_test = min(int(spec.E * spec.test_frac), rest.shape[0])
+    train = np.vstack([cover, rest[n_test:]])
+    train = train[rs.permutation(train.shape[0])].astype(np.int32)
+    r = (rs.random(train.shape[0]) < spec.pos_frac).astype(np.int32)
+    counts = np.zeros((train.shape[0], 2), dtype=np.int32)
+    counts[np.arange(train.shape[0]), r] = 1
+    return np.ascontiguousarray(train), counts

@@ -30,6 +30,7 @@ NATIVE_INGEST = True   # get_traintest's native reader for canonical files (inge
 
 class Model:
     def __init__(self, device=None):
+        self._links_version = 0
         self._fold = None               # native parse backing the lazy link dicts (ingest.py)
         self._fold_fresh = [False, False]
         self.ntheta = []
@@ -53,7 +54,6 @@ class Model:
         self._device = device
         self._engine = None
         self._engine_key = None
-        self._links_version = 0
         self._host_fresh = True   # host lists hold the newest parameters
         self._dev_fresh = False   # device tensors hold the newest parameters
 
@@ -93,7 +93,10 @@ class Model:
     # ---------------------------------------------- link tables (lazy after a native parse)
     # After get_traintest's native reader, `links` / `nlinks` / `test_links` are built as the
     # reference's dicts on first access; until a caller has touched them the engine and the
-    # counts below read the parsed arrays directly.
+    # counts below read the parsed arrays directly.  The device copy of a link table is made
+    # when the engine is built: assigning a new table (the setters) or calling
+    # `links_changed()` after editing a dict in place makes the next call rebuild it (the
+    # reference re-reads the dicts on every call, :987, :959).
     @property
     def links(self):
         if self._links is None:
@@ -105,6 +108,7 @@ class Model:
     def links(self, value):
         self._links = value
         self._fold_fresh[0] = False
+        self._links_version += 1        # a new table: the engine re-reads it
 
     @property
     def test_links(self):
@@ -117,6 +121,7 @@ class Model:
     def test_links(self, value):
         self._test_links = value
         self._fold_fresh[1] = False
+        self._links_version += 1
 
     @property
     def nlinks(self):
@@ -127,6 +132,10 @@ class Model:
     @nlinks.setter
     def nlinks(self, value):
         self._nlinks = value
+
+    def links_changed(self):
+        """Declare an in-place edit of `links` / `test_links`: the device tables are rebuilt."""
+        self._links_version += 1
 
     def _link_arrays(self, which):
         """(ids int32[E][3] in key order, counts int32[E][R]) of the train (0) / test (1) links."""
@@ -366,6 +375,12 @@ class Model:
             ids = [int(id1), int(id2), int(id3)]
         except ValueError:
             ids = [self.gene_id[id1], self.gene_id[id2], self.gene_id[id3]]
+        # the reference indexes the theta list (:537): an id >= P raises IndexError and a
+        # negative id counts from the end; the device kernel is only ever handed ids in [0, P)
+        for n, g in enumerate(ids):
+            if not -self.P <= g < self.P:
+                raise IndexError("list index out of range")
+            ids[n] = g % self.P
         eng = self._push()
         return float(eng.predict(np.array([ids], dtype=np.int32))[0, 0])
 
@@ -432,9 +447,10 @@ class Model:
         try:
             if name_file is None:
                 name_file = "out.txt"
-            data = self.to_string()
+            # the file is created before the text is built (:898-899): if to_string raises, an
+            # empty file stays behind, which the CLI's resume rule (:1256) then skips
             with codecs.open(name_file, encoding='utf-8', mode="w+") as fileref:
-                fileref.write(data)
+                fileref.write(self.to_string())
         except IOError:
             print("I/O error")
 
