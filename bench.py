@@ -104,6 +104,31 @@ def spawn_ranks(n):
     return rc
 
 
+KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, d, c, M0 on FP64 MFMA)",
+                "pass_b": "pass_kernel<%d, PASS_B> (streams 1/2: M1, M2; S partials)",
+                "fin": "fin_kernel<%d> (per-gene X contractions, theta and p update)"}
+
+
+def kernel_work(plan, K, P, R, B, E_obs):
+    """Algorithmic (FLOPs, HBM bytes) of one launch of each kernel of the pivot-run iteration
+    (DESIGN.md "Roofline accounting"): per observation 2K^2 (Z) + 2K (d) + 2K^2 (M) in pass A,
+    2 x 2K^2 (M1, M2) in pass B; per pivot gene 2K^3 (V, S partial, each X); bytes = the
+    records, c, partial rows and parameters each launch must move once."""
+    K2, K3 = K * K, K ** 3
+    rows0, rows = plan["rows_stream0"], plan["rows"]
+    prows = plan["partial_rows"]
+    prow0 = plan["partial_rows_stream0"]
+    genes_a = plan["v_genes"]
+    params = 8.0 * (P * K + R * K3)
+    a_fl = E_obs * (4.0 * K2 + 2.0 * K) + genes_a * 2.0 * K3
+    a_by = 16.0 * rows0 + 8.0 * rows0 + 8.0 * K2 * prow0 + params
+    b_fl = E_obs * 4.0 * K2 + prow0 * 2.0 * K3
+    b_by = 16.0 * (rows - rows0) + 8.0 * (rows - rows0) + 8.0 * K2 * prows + params
+    f_fl = 3.0 * R * P * 2.0 * K3 + 3.0 * R * K3
+    f_by = 8.0 * K2 * prows + 2.0 * params
+    return {"pass_a": (a_fl * B, a_by * B), "pass_b": (b_fl * B, b_by * B), "fin": (f_fl * B, f_by * B)}
+
+
 def make_fold(P, E, rank):
     from trigenicinteractionpredictor_amd.data import FoldSpec, write_fold
     d = tempfile.mkdtemp(prefix="mmsbm_bench_r%d_" % rank)
@@ -244,7 +269,7 @@ def main():
             dist.init_process_group(args.backend)
 
     from trigenicinteractionpredictor_amd import EMEngine, Model
-    from trigenicinteractionpredictor_amd.layout import links_to_arrays, build_obs
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays, n_observations
 
     import contextlib
     import io
@@ -270,13 +295,14 @@ def main():
         from trigenicinteractionpredictor_amd.linkshard import LinkShardedEM, shard_links
         runner = LinkShardedEM(eng, ids, counts, tids, tcounts)
         lo, hi = shard_links(ids.shape[0], world, rank)
-        E_obs = int(build_obs(ids[lo:hi], counts[lo:hi]).n_obs)   # this rank's E-step launch
+        E_obs = n_observations(counts[lo:hi])      # this rank's observations
     else:
         eng.set_links(0, ids, counts)
         eng.set_links(1, tids, tcounts)
         runner = eng
-        E_obs = int(build_obs(ids, counts).n_obs)
+        E_obs = n_observations(counts)
     runner.upload(np.stack(thetas), np.stack(prs))
+    plan = eng.plan_info(0)
 
     # per-kernel in-loop times come from event pairs in the (untimed) warmup iterations: an
     # event record between two dependent launches costs the loop ~1-2 us, so the timed region
@@ -284,9 +310,7 @@ def main():
     eng.timing(0 if args.no_events else args.event_stride)
     runner.iterate(args.warmup)
     torch.cuda.synchronize(dev)
-    est_ms, est_n = eng.timing_result("estep")
-    m1_ms, _ = eng.timing_result("m1")
-    m2_ms, _ = eng.timing_result("m2")
+    in_loop = {k: eng.timing_result(k) for k in eng.KERNELS}
     eng.timing(False)
     if world > 1:
         dist.barrier()
@@ -297,9 +321,9 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    # the dominant kernel alone, back to back on the same stream (per-launch duration for the
-    # roofline; the in-loop events above also time the dependent-launch boundary around it)
-    est_b2b_ms = eng.time_estep(args.roofline_launches)
+    # each kernel of the iteration alone, back to back on the launch stream (per-launch duration
+    # for the roofline; the in-loop events above also time the dependent-launch boundary)
+    b2b = {k: eng.time_kernel(k, args.roofline_launches) for k in eng.KERNELS}
     elapsed = t1 - t0
     L = torch.from_numpy(runner.loglik(0)).to(coll)
     if world > 1:
@@ -309,30 +333,29 @@ def main():
         gathered = [torch.empty_like(L) for _ in range(world)]
         dist.all_gather(gathered, L)       # RCCL gather of final likelihoods
         L_all = torch.cat(gathered).cpu().numpy()
-        n_gathered = int(L_all.shape[0])
     else:
         L_all = L.cpu().numpy()
-        n_gathered = int(L_all.shape[0])
+    n_gathered = int(L_all.shape[0])
 
     if rank == 0:
         iters_total = args.steps * B * (1 if links_mode else world)
         value = iters_total / elapsed
-        # roofline of the dominant kernel (the E-step), per launch; SURVEY.md §8d figures.
-        # Fused path (FP64 MFMA): the E-step launch does Y, Z, W and S = 8 K^3 per observation;
-        # VALU path: the E-step does Y, Z, W = 6 K^3 (S is M1's 2 K^3).
-        fused = eng.fused                 # E-step + S in one launch (K <= 12)
-        kind = eng.fused_kind             # 0 VALU, 1/2 fused MFMA, 3 large-K MFMA E-step
-        est_avg_s = est_b2b_ms / 1e3
-        flops = (8.0 if fused else 6.0) * K ** 3 * E_obs * B
-        hbm_bytes = (16.0 * E_obs + 16.0 * host.P * K + 24.0 * K ** 3 * 2) * B
-        achieved_tf = flops / est_avg_s / 1e12
+        work = kernel_work(plan, K, host.P, 2, B, E_obs)
+        dom = max(b2b, key=b2b.get)          # the dominant kernel of the iteration
+        dom_s = b2b[dom] / 1e3
+        fl, by = work[dom]
+        tf, gbs = fl / dom_s / 1e12, by / dom_s / 1e9
+        f_mfma, f_hbm = tf / FP64_PEAK_TFLOPS, gbs / HBM_PEAK_GBS
+        bound = "mfma" if f_mfma >= f_hbm else "hbm"
         traffic = None
-        pmc = os.path.join(REPO, "profiles", "pmc_estep_K%d.json" % K)
+        pmc = os.path.join(REPO, "profiles", "pmc_r02_K%d.json" % K)
         if os.path.exists(pmc):
             with open(pmc) as f:
                 rec = json.load(f)
-            if rec.get("E_obs") == E_obs and rec.get("B") == B and rec.get("fused") == fused:
-                traffic = rec.get("hbm_bytes_per_launch")
+            if rec.get("E_obs") == E_obs and rec.get("B") == B:
+                traffic = rec.get("hbm_bytes_per_launch", {}).get(dom)
+        iter_s = elapsed / args.steps
+        s8d_flops = 8.0 * K ** 3 * E_obs * B      # SURVEY.md 8d's credit for one iteration
         line = {
             "metric": "EM-iterations/sec + final log-likelihood, fold0 K=%d" % K,
             "value": value,
@@ -356,21 +379,28 @@ def main():
             "gathered_samples": n_gathered,
             "final_loglik": float(L_all[0]),
             "final_loglik_best": float(L_all.max()),
-            "roofline": {"bound": "mfma" if kind else "fp64-valu", "achieved": achieved_tf,
-                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": {1: "emx_kernel<%d> (E-step + S, FP64 MFMA)",
-                                    2: "eml_kernel<%d> (E-step + S, FP64 MFMA, lean)",
-                                    3: "emb_kernel<%d> (E-step, FP64 MFMA; S in m1x_kernel)"}.get(
-                                        kind, "estep_kernel<%d> (VALU)") % K,
-                         "avg_launch_us": est_avg_s * 1e6,
-                         "algorithmic_flops_per_launch": flops,
-                         "hbm": {"achieved": hbm_bytes / est_avg_s / 1e9, "peak": HBM_PEAK_GBS,
-                                 "unit": "GB/s", "frac": hbm_bytes / est_avg_s / 1e9 / HBM_PEAK_GBS,
-                                 "algorithmic_bytes_per_launch": hbm_bytes}},
-            "kernel_us": {"estep": est_ms * 1e3 / max(est_n, 1), "estep_back_to_back": est_avg_s * 1e6,
-                          "m1": m1_ms * 1e3 / max(est_n, 1),
-                          "m2": m2_ms * 1e3 / max(est_n, 1)},
+            "roofline": {"bound": bound,
+                         "achieved": tf if bound == "mfma" else gbs,
+                         "peak": FP64_PEAK_TFLOPS if bound == "mfma" else HBM_PEAK_GBS,
+                         "unit": "TFLOP/s" if bound == "mfma" else "GB/s",
+                         "frac": f_mfma if bound == "mfma" else f_hbm,
+                         "traffic": traffic,
+                         "kernel": KERNEL_NAMES[dom] % K,
+                         "avg_launch_us": dom_s * 1e6,
+                         "algorithmic_flops_per_launch": fl,
+                         "algorithmic_bytes_per_launch": by,
+                         "mfma": {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "frac": f_mfma},
+                         "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "frac": f_hbm}},
+            "iteration": {"us": iter_s * 1e6,
+                          "s8d_credit_flops": s8d_flops,
+                          "s8d_effective_tflops": s8d_flops / iter_s / 1e12,
+                          "note": "SURVEY 8d credits 8 K^3 FLOPs per observation (the reference's "
+                                  "per-link lattice); the pivot-run factorisation executes "
+                                  "O(K^2) per observation + O(K^3) per gene (DESIGN.md)"},
+            "kernel_us": {k: {"back_to_back": b2b[k] * 1e3,
+                              "in_loop": in_loop[k][0] * 1e3 / max(in_loop[k][1], 1)}
+                          for k in eng.KERNELS},
+            "plan": plan,
             "cpu_baseline": cpu_rec,
         }
         if cpu_rec is not None:

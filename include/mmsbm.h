@@ -11,26 +11,21 @@
  * Conventions
  *  - every call returns MMSBM_OK (0) or a negative MMSBM_ERR_* code;
  *    mmsbm_last_error() returns the message of the last failure (thread-local);
- *  - all array pointers are DEVICE pointers (memory owned by the caller, e.g.
- *    PyTorch tensors) unless the parameter name ends in _host;
- *  - kernels are enqueued on the caller's hipStream_t (passed as void*); only
- *    setup calls (set_links / set_genes) synchronise;
- *  - a context is not thread-safe: one host thread per context, one process
- *    per GPU.
+ *  - pointers whose name ends in _host are HOST arrays; every other array
+ *    pointer is a DEVICE pointer (memory owned by the caller, e.g. PyTorch
+ *    tensors);
+ *  - kernels are enqueued on the caller's hipStream_t (passed as void*); the
+ *    setup calls (set_links, set_degree, set_workspace) synchronise;
+ *  - every call runs on the context's device and restores the caller's current
+ *    device on return;
+ *  - a context is not thread-safe: one host thread per context.
  *
  * Device layouts
- *  - obs    int32[n_obs_pad][4] = (id1, id2, id3, n): one row per OBSERVED
- *           (link, rating) pair, ids in the reference's string-sorted key order
- *           (:349-358), n = links[key][r] (:360-368).  Rows are grouped by
- *           rating r; every group starts on a multiple of MMSBM_TILE and is
- *           padded with (0,0,0,0) rows (weight 0, contributes exactly 0).
  *  - theta  f64[B][P][K]          membership vectors of B batched samples (:117-121)
  *  - pr     f64[B][R][K][K][K]    rating-major copy of the reference's
  *           pr[K][K][K][R] (:124-139)
- *  - gene CSR: gene_ptr int32[P+1], gene_inc int32[nnz] with entries
- *           obs_row*3 + slot, listing every (observation, slot) of gene g in
- *           ascending order; deg int32[P] = the reference's `counter`
- *           (:986-994: one per link slot, independent of the counts).
+ *  The engine's own work plan (observation streams ordered by each slot's gene,
+ *  DESIGN.md) is built inside mmsbm_set_links from the host link table.
  */
 #ifndef MMSBM_H
 #define MMSBM_H
@@ -48,7 +43,7 @@ extern "C" {
                                      ZeroDivisionError at :1018 */
 #define MMSBM_ERR_UNSUPPORTED -4  /* shape outside the compiled kernel set */
 
-#define MMSBM_TILE 256            /* observations per workgroup tile */
+#define MMSBM_CHUNK 4             /* observations per MFMA k-step (one pivot gene each) */
 #define MMSBM_MAX_K 32
 #define MMSBM_SET_TRAIN 0         /* `links` (:57) */
 #define MMSBM_SET_TEST 1          /* `test_links` (:61) */
@@ -56,7 +51,7 @@ extern "C" {
 typedef struct mmsbm_ctx mmsbm_ctx;
 
 int mmsbm_version(void);
-int mmsbm_tile(void);
+int mmsbm_chunk(void);
 const char *mmsbm_last_error(void);
 
 /* Context = one GPU + one problem shape.  Replaces the per-process `Model()`
@@ -68,23 +63,22 @@ int mmsbm_destroy(mmsbm_ctx *ctx);
  * (independent restarts, :1253), P genes (:413), eps (:88). */
 int mmsbm_set_shape(mmsbm_ctx *ctx, int32_t K, int32_t R, int32_t B, int32_t P, double eps);
 
-/* Device edge list of one link set (MMSBM_SET_TRAIN = `links`,
- * MMSBM_SET_TEST = `test_links`), built by the host from get_traintest's
- * dicts (:321-423).  seg_host[R+1]: start row of each rating group
- * (seg_host[R] = n_obs_pad); every entry a multiple of MMSBM_TILE. */
-int mmsbm_set_links(mmsbm_ctx *ctx, int32_t which, const int32_t *obs, int64_t n_obs_pad,
-                    const int64_t *seg_host);
+/* One link set (MMSBM_SET_TRAIN = `links`, MMSBM_SET_TEST = `test_links`) as the
+ * reference holds it after get_traintest (:321-423), in dict insertion order:
+ * ids_host[E][3] = the key's gene ids in its string-sorted order ('10_2_9' ->
+ * 10, 2, 9; :349-358), counts_host[E][R] = links[key] (:360-368).  Builds the
+ * device work plan.  For the train set it also computes the degree (the
+ * reference's `counter`, :986-994: one per link slot) unless mmsbm_set_degree
+ * fixed it.  Invalidates the workspace (query mmsbm_workspace_bytes again). */
+int mmsbm_set_links(mmsbm_ctx *ctx, int32_t which, const int32_t *ids_host,
+                    const int32_t *counts_host, int64_t E);
 
-/* Gene incidence CSR of the TRAIN set for the theta M-step (:1016-1018).  Call after
- * mmsbm_set_links(MMSBM_SET_TRAIN) (re-setting the train links requires calling it again).
- * The engine inverts it once on the device: every observation's three responsibility rows
- * are then written straight to their gene's contiguous CSR run.
- * Validates deg > 0 for every gene (copies deg to the host once); a zero
- * returns MMSBM_ERR_ZERO_DEGREE and makes mmsbm_iterate fail the same way. */
-int mmsbm_set_genes(mmsbm_ctx *ctx, const int32_t *gene_ptr, const int32_t *gene_inc,
-                    int64_t nnz, const int32_t *deg);
+/* deg_host[P]: the degree the M-step divides by (:1016-1018) — for a
+ * link-sharded rank the counter over ALL train links, not its own block.  A
+ * zero makes mmsbm_iterate / mmsbm_mstep fail with MMSBM_ERR_ZERO_DEGREE. */
+int mmsbm_set_degree(mmsbm_ctx *ctx, const int32_t *deg_host);
 
-/* Scratch the engine needs (responsibility rows, per-tile partial sums). */
+/* Scratch the engine needs (c per observation, partial rows, S partials). */
 int mmsbm_workspace_bytes(const mmsbm_ctx *ctx, int64_t *bytes);
 int mmsbm_set_workspace(mmsbm_ctx *ctx, void *ws, int64_t bytes);
 
@@ -97,16 +91,16 @@ int mmsbm_iterate(mmsbm_ctx *ctx, double *theta, double *pr, int32_t n_iters, vo
 int mmsbm_loglik(mmsbm_ctx *ctx, int32_t which, const double *theta, const double *pr,
                  double *out, void *stream);
 
-/* P(r = 1) for n rows of ids int32[n][3] into out[B][n] (device).
- * Replaces Model.do_prediction (:530-547), used by calculate_test_set_results
- * (:557-569). */
+/* P(r = 1) for n rows of ids int32[n][3] into out[B][n] (device); an id outside
+ * [0, P) gives NaN.  Replaces Model.do_prediction (:530-547), used by
+ * calculate_test_set_results (:557-569). */
 int mmsbm_predict(mmsbm_ctx *ctx, const int32_t *ids, int64_t n, const double *theta,
                   const double *pr, double *out, void *stream);
 
 /* Link-sharded iteration (single sample over N ranks): each rank's context
- * holds 1/N of the train links (mmsbm_set_links) and the GLOBAL degree (mmsbm_set_genes' deg).
+ * holds 1/N of the train links (mmsbm_set_links) and the GLOBAL degree (mmsbm_set_degree).
  * Step 1, the accumulation half of make_iteration (:986-1012) over this rank's links:
- *   nth[B][P][K]   = per gene, the sum of its local c-scaled (Y | Z | W) rows (theta not applied)
+ *   nth[B][P][K]   = per gene, the sum of its c-scaled responsibility marginals (theta not applied)
  *   S[B][R][K^3]   = the S lattice sums,  npr = p S.
  * The caller sums nth and S over ranks (one all-reduce of one buffer), then step 2 applies the
  * M-step (:1016-1028): theta <- theta nth / deg, p_r <- p_r S_r / (eps + sum_r p_r S_r).
@@ -116,26 +110,25 @@ int mmsbm_accumulate(mmsbm_ctx *ctx, const double *theta, const double *pr, doub
 int mmsbm_mstep(mmsbm_ctx *ctx, double *theta, double *pr, const double *nth, const double *S,
                 void *stream);
 
-/* Which E-step path mmsbm_iterate runs: 1 = fused FP64-MFMA KR-image kernel (E-step and S
- * accumulation in one kernel, then M2; K <= 10), 2 = the lean fused kernel (K = 11, 12, or
- * MMSBM_ESTEP=5), 3 = the large-K FP64-MFMA pair (E-step kernel, S-accumulation kernel, M2;
- * 13 <= K <= 32), 0 = the VALU E-step + M1 + M2 (MMSBM_ESTEP=1/2). */
-int mmsbm_fused(const mmsbm_ctx *ctx, int32_t *fused);
+/* Measurement: info[10] = observations, plan rows (3 streams), stream-0 rows, stream-0
+ * workgroups, stream-1/2 workgroups, S-partial workgroups, partial rows, most genes per
+ * stream-0 workgroup, V genes over all stream-0 workgroups, stream-0 partial rows. */
+int mmsbm_plan_info(const mmsbm_ctx *ctx, int32_t which, int64_t *info);
 
 /* Kernel timing for measurement (bench.py): with stride n > 0, mmsbm_iterate records a HIP
  * event pair on the launch stream around every kernel of every n-th iteration (kernel ids:
- * 0 E-step, 1 M1 = S accumulation + theta gather, 2 M2 = p update); 0 disables.
- * mmsbm_timing resets the counters; mmsbm_timing_result waits for the last event and returns
- * the summed device time (ms) and the number of timed launches of that kernel. */
+ * 0 pass A = stream 0, 1 pass B = streams 1/2 + S partials, 2 fin = theta / p update);
+ * 0 disables.  mmsbm_timing resets the counters; mmsbm_timing_result waits for the last event
+ * and returns the summed device time (ms) and the number of timed launches of that kernel. */
 int mmsbm_timing(mmsbm_ctx *ctx, int32_t stride);
-
-/* Measurement: n back-to-back launches of the E-step kernel mmsbm_iterate would run (the fused
- * kernel, or the VALU E-step) on the current theta / pr, between one HIP event pair on
- * `stream`; *avg_ms = elapsed / n.  The E-step only reads theta / pr, so the parameters are
- * unchanged.  Synchronises the stream. */
-int mmsbm_time_estep(mmsbm_ctx *ctx, double *theta, double *pr, int32_t n, void *stream,
-                     double *avg_ms);
 int mmsbm_timing_result(mmsbm_ctx *ctx, int32_t kernel, double *total_ms, int64_t *count);
+
+/* Measurement: n back-to-back launches of kernel `kernel` (ids as above) on the current theta /
+ * pr, between one HIP event pair on `stream`; *avg_ms = elapsed / n.  The passes only read
+ * theta / pr and fin runs in its sums-out mode into workspace scratch, so the parameters are
+ * unchanged.  Synchronises the stream. */
+int mmsbm_time_kernel(mmsbm_ctx *ctx, int32_t kernel, double *theta, double *pr, int32_t n,
+                      void *stream, double *avg_ms);
 
 #ifdef __cplusplus
 }

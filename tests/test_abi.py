@@ -40,8 +40,8 @@ def test_python_binding_covers_the_header():
 
 def test_constants_and_error_string(lib):
     from trigenicinteractionpredictor_amd import _lib
-    assert lib.mmsbm_tile() == 256
-    assert lib.mmsbm_version() >= 1
+    assert lib.mmsbm_chunk() == 4
+    assert lib.mmsbm_version() >= 2
     # argument validation happens before any device call
     assert lib.mmsbm_create(0, None) == _lib.MMSBM_ERR_INVALID
     assert b"null" in lib.mmsbm_last_error()

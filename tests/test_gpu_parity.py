@@ -116,88 +116,56 @@ def test_against_c_oracle(tmp_path, K, P, E, iters):
     np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
 
 
-@pytest.mark.parametrize("K", [3, 10, 13])
-@pytest.mark.parametrize("groups", ["1", "5", "2048"])
-def test_s_accumulation_workgroup_splits(tmp_path, monkeypatch, K, groups):
-    """M1 with one workgroup (many windows, every rating boundary inside it), a few, and one
-    tile per workgroup: all equal the oracle."""
-    monkeypatch.setenv("MMSBM_SACC_WGS", groups)
-    tr, te = _fold(tmp_path, 300, 12000, seed=K, multi_frac=0.05, both_frac=0.02)
+@pytest.mark.parametrize("units", ["1,1", "3,5", None])
+@pytest.mark.parametrize("K", [3, 10, 16])
+def test_work_plan_splits_match_oracle(tmp_path, monkeypatch, K, units):
+    """Unit / workgroup splits of the observation streams (csrc/plan.h): two units in all (every
+    pivot run of a stream in one wave, up to lmax chunks), a few, and the default; K=16 has no
+    zero V rows (16 = 4 b-tiles), K=3 / K=10 pad."""
+    if units is None:
+        monkeypatch.delenv("MMSBM_UNITS", raising=False)
+    else:
+        monkeypatch.setenv("MMSBM_UNITS", units)
+    tr, te = _fold(tmp_path, 300, 6000, seed=K, multi_frac=0.05, both_frac=0.02)
     m = _gpu_model(tr, te)
     random.seed(K + 1)
     m.initialize_parameters(K)
     theta0, pr0 = np.array(m.theta), np.array(m.pr)
     m.make_iterations(2)
-    th_o, pr_o, L_o, _ = _oracle_run(m, theta0, pr0, 2)
+    th_o, pr_o, L_o, LT_o = _oracle_run(m, theta0, pr0, 2)
     np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
+    np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
 
 
-def test_estep_variants_agree(tmp_path, monkeypatch):
-    """The E-step variants (fused MFMA default, 2-lane VALU + M1, 4-lane VALU + M1) all match
-    the oracle."""
-    tr, te = _fold(tmp_path, 400, 8000, seed=21, multi_frac=0.05)
-    for variant in ("0", "1", "2"):
-        monkeypatch.setenv("MMSBM_ESTEP", variant)
-        m = _gpu_model(tr, te)
-        random.seed(3)
-        m.initialize_parameters(8)
-        theta0, pr0 = np.array(m.theta), np.array(m.pr)
-        m.make_iterations(2)
-        th_o, pr_o, _, _ = _oracle_run(m, theta0, pr0, 2)
-        np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
-        np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
-
-
-@pytest.mark.parametrize("K", [3, 10, 12])
-@pytest.mark.parametrize("groups", ["1", "256"])
-def test_lean_fused_estep_matches_oracle(tmp_path, monkeypatch, K, groups):
-    """MMSBM_ESTEP=5 (fused E-step without the KR image) matches the oracle:
-    one workgroup for everything and the default split, ragged last groups, padded lanes."""
-    tr, te = _fold(tmp_path, 300, 5000, seed=40 + K, multi_frac=0.05, both_frac=0.02)
-    monkeypatch.setenv("MMSBM_ESTEP", "5")
-    monkeypatch.setenv("MMSBM_SACC_WGS", groups)
+@pytest.mark.parametrize("K,P,E", [(30, 3000, 4000), (12, 4000, 3000), (4, 30, 1500), (32, 40, 900)])
+def test_short_and_long_pivot_runs_match_oracle(tmp_path, K, P, E):
+    """Many genes with one or two observations each (every chunk a new pivot gene: stream-0
+    workgroups capped by their V table, one partial row per chunk) and few genes with very long
+    runs (runs split over units and workgroups, partial rows summed per gene)."""
+    tr, te = _fold(tmp_path, P, E, seed=K + P, multi_frac=0.05, both_frac=0.05)
     m = _gpu_model(tr, te)
     random.seed(K)
     m.initialize_parameters(K)
     theta0, pr0 = np.array(m.theta), np.array(m.pr)
     m.make_iterations(2)
-    assert m._engine.fused
-    th_o, pr_o, L_o, _ = _oracle_run(m, theta0, pr0, 2)
+    info = m._engine.plan_info()
+    assert info["genes_per_wg_max"] >= 1 and info["partial_rows"] >= 1
+    th_o, pr_o, L_o, LT_o = _oracle_run(m, theta0, pr0, 2)
     np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
+    np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
 
 
-@pytest.mark.parametrize("K,kind", [(2, 1), (10, 1), (11, 2), (12, 2), (13, 3), (32, 3)])
-def test_default_estep_kernel_choice(tmp_path, K, kind):
-    """Default dispatch: KR-image fused kernel up to K=10, lean fused kernel at K=11/12 (the
-    KR-image kernel only fits 4 waves there), large-K MFMA E-step + S kernels above; each
-    matches the oracle."""
-    tr, te = _fold(tmp_path, 200, 3000, seed=60 + K, multi_frac=0.05)
-    m = _gpu_model(tr, te)
-    random.seed(K)
-    m.initialize_parameters(K)
-    theta0, pr0 = np.array(m.theta), np.array(m.pr)
-    m.make_iterations(2)
-    assert m._engine.fused_kind == kind
-    th_o, pr_o, _, _ = _oracle_run(m, theta0, pr0, 2)
-    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
-    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
-
-
-@pytest.mark.parametrize("K,P,E,B", [(13, 200, 3000, 1), (17, 150, 2500, 2), (24, 120, 2000, 1),
-                                     (29, 100, 1500, 1), (32, 100, 1200, 2)])
-@pytest.mark.parametrize("groups", ["1", "256"])
-def test_large_k_mfma_path_matches_oracle(tmp_path, monkeypatch, K, P, E, B, groups):
-    """emb_kernel (p_r staged in a-chunks above K ~ 22, lockstep rounds, idle waves in the last
-    round) + m1x_kernel (4 x 4 (a, b) tiles per wave) against the oracle, per sample of a batch;
-    one workgroup for everything and the default split."""
+@pytest.mark.parametrize("K,P,E,B", [(2, 200, 3000, 3), (13, 200, 3000, 1), (17, 150, 2500, 2),
+                                     (24, 120, 2000, 1), (29, 100, 1500, 1), (32, 100, 1200, 2)])
+def test_batched_engine_matches_oracle(tmp_path, K, P, E, B):
+    """EMEngine with B batched samples against the oracle, per sample, at K up to 32."""
     from oracle import c_oracle
     from trigenicinteractionpredictor_amd import EMEngine
     from trigenicinteractionpredictor_amd.layout import links_to_arrays
-    monkeypatch.setenv("MMSBM_SACC_WGS", groups)
     tr, te = _fold(tmp_path, P, E, seed=70 + K, multi_frac=0.05, both_frac=0.02)
     m = _gpu_model(tr, te)
     random.seed(K)
@@ -209,42 +177,23 @@ def test_large_k_mfma_path_matches_oracle(tmp_path, monkeypatch, K, P, E, B, gro
     eng = EMEngine(K, m.P, B=B)
     ids, counts = links_to_arrays(m.links)
     eng.set_links(0, ids, counts)
-    assert eng.fused_kind == 3
     eng.upload(np.stack(thetas), np.stack(prs))
     eng.iterate(2)
     th, pr = eng.download()
+    L = eng.loglik(0)
     for b in range(B):
         th_o, pr_o = thetas[b], prs[b]
         for _ in range(2):
             th_o, pr_o = c_oracle.make_iteration(ids, counts, th_o, pr_o)
         np.testing.assert_allclose(th[b], th_o, rtol=RTOL, atol=ATOL)
         np.testing.assert_allclose(pr[b], pr_o, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(L[b], c_oracle.loglik(ids, counts, th_o, pr_o), rtol=RTOL)
 
 
-def test_large_k_valu_variant_still_matches(tmp_path, monkeypatch):
-    monkeypatch.setenv("MMSBM_ESTEP", "1")
-    tr, te = _fold(tmp_path, 150, 2000, seed=5, multi_frac=0.05)
-    m = _gpu_model(tr, te)
-    random.seed(2)
-    m.initialize_parameters(20)
-    theta0, pr0 = np.array(m.theta), np.array(m.pr)
-    m.make_iterations(2)
-    assert m._engine.fused_kind == 0
-    th_o, pr_o, _, _ = _oracle_run(m, theta0, pr0, 2)
-    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
-    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
-
-
-@pytest.mark.parametrize("wgs", ["64", None])
-def test_batched_samples_match_single_runs(tmp_path, monkeypatch, wgs):
-    """A sample's result does not depend on its batch-mates: bitwise when MMSBM_SACC_WGS pins
-    the per-sample workgroup count; by default the count scales as 256 / B, so a batch splits
-    each sample's observations into other (fixed) ranges and the sums agree to rounding."""
+def test_batched_samples_match_single_runs_bitwise(tmp_path):
+    """A sample's bits do not depend on its batch-mates or the batch size: the work plan is
+    the same for every B (so restart sharding over 1 or 8 GPUs gives identical samples)."""
     from trigenicinteractionpredictor_amd import EMEngine, Model
-    if wgs is not None:
-        monkeypatch.setenv("MMSBM_SACC_WGS", wgs)
-    else:
-        monkeypatch.delenv("MMSBM_SACC_WGS", raising=False)
     from trigenicinteractionpredictor_amd.layout import links_to_arrays
     tr, te = _fold(tmp_path, 200, 2000, seed=3)
     m = Model()
@@ -269,14 +218,9 @@ def test_batched_samples_match_single_runs(tmp_path, monkeypatch, wgs):
         single.K = K
         single.theta, single.pr = thetas[s].tolist(), prs[s].tolist()
         single.make_iterations(4)
-        if wgs is not None:
-            np.testing.assert_array_equal(np.array(single.theta), th_b[s])
-            np.testing.assert_array_equal(np.array(single.pr), pr_b[s])
-            assert single.compute_likelihood() == L_b[s]
-        else:
-            np.testing.assert_allclose(np.array(single.theta), th_b[s], rtol=1e-10, atol=1e-300)
-            np.testing.assert_allclose(np.array(single.pr), pr_b[s], rtol=1e-10, atol=1e-300)
-            assert abs(single.compute_likelihood() - L_b[s]) <= 1e-10 * abs(L_b[s])
+        np.testing.assert_array_equal(np.array(single.theta), th_b[s])
+        np.testing.assert_array_equal(np.array(single.pr), pr_b[s])
+        assert single.compute_likelihood() == L_b[s]
 
 
 def test_bitwise_reproducible(tmp_path):

@@ -13,7 +13,7 @@ import pytest
 
 from golden_util import cases, load
 from trigenicinteractionpredictor_amd.data import FoldSpec, write_fold
-from trigenicinteractionpredictor_amd.layout import TILE, build_gene_csr, build_obs, links_to_arrays
+from trigenicinteractionpredictor_amd.layout import links_to_arrays, n_observations
 from trigenicinteractionpredictor_amd.model import Model
 
 CASES = cases()
@@ -67,52 +67,13 @@ def test_metrics_ties_counted_as_not_greater():
     assert auc == 1 / 4
 
 
-def test_layout_rows_and_padding():
+def test_link_arrays_keep_key_order_and_counts():
     links = {"0_1_2": [1, 0], "10_2_9": [0, 2], "3_3_4": [2, 1], "1_5_6": [0, 1]}
     ids, counts = links_to_arrays(links)
     assert ids[1].tolist() == [10, 2, 9]         # string-sorted key order is kept
-    lay = build_obs(ids, counts, by_gene=False)
-    assert lay.seg[0] == 0 and all(s % TILE == 0 for s in lay.seg)
-    real = lay.obs[lay.link_of_row >= 0]
-    assert lay.n_obs == 5
-    # r = 0 group first (links 0, 2), then r = 1 (links 1, 2, 3), each in link order
-    assert lay.link_of_row[lay.link_of_row >= 0].tolist() == [0, 2, 1, 2, 3]
-    assert real[:, 3].tolist() == [1, 2, 2, 1, 1]
-    pad = lay.obs[lay.link_of_row < 0]
-    assert not pad.any()
-
-
-def test_layout_by_gene_orders_each_rating_by_slot0_gene():
-    links = {"0_1_2": [1, 0], "10_2_9": [0, 2], "3_3_4": [2, 1], "1_5_6": [0, 1]}
-    ids, counts = links_to_arrays(links)
-    lay = build_obs(ids, counts)
-    # r = 0: links 0 (gene 0), 2 (gene 3); r = 1: links 3 (gene 1), 2 (gene 3), 1 (gene 10)
-    assert lay.link_of_row[lay.link_of_row >= 0].tolist() == [0, 2, 3, 2, 1]
-    real = lay.obs[lay.link_of_row >= 0]
-    assert real[:, 0].tolist() == [0, 3, 1, 3, 10]
-    assert real[:, 3].tolist() == [1, 2, 1, 1, 2]
-
-
-def test_gene_csr_lists_every_incidence_and_counter():
-    rng = np.random.default_rng(3)
-    P, E = 40, 300
-    ids = rng.integers(0, P, size=(E, 3)).astype(np.int32)
-    counts = rng.integers(0, 3, size=(E, 2)).astype(np.int32)
-    counts[counts.sum(1) == 0, 0] = 1
-    lay = build_obs(ids, counts)
-    csr = build_gene_csr(lay, ids, P)
-    assert csr.ptr[-1] == csr.inc.size == 3 * lay.n_obs
-    for g in range(P):
-        ent = csr.inc[csr.ptr[g]:csr.ptr[g + 1]]
-        assert (np.diff(ent) > 0).all()
-        rows, slots = ent // 3, ent % 3
-        assert (lay.obs[rows, slots] == g).all()
-    # deg == the reference's counter (:986-994): one per link slot, counts ignored
-    ref = [0] * P
-    for row in ids:
-        for g in row:
-            ref[g] += 1
-    assert csr.deg.tolist() == ref
+    assert ids[2].tolist() == [3, 3, 4]          # a repeated gene keeps both slots
+    assert counts.tolist() == [[1, 0], [0, 2], [2, 1], [0, 1]]
+    assert n_observations(counts) == 5
 
 
 def test_fold_splits_are_complementary(tmp_path):

@@ -22,18 +22,20 @@ MMSBM_ERR_ZERO_DEGREE = -3
 MMSBM_ERR_UNSUPPORTED = -4
 SET_TRAIN = 0
 SET_TEST = 1
+CHUNK = 4
+MAX_K = 32
 
 # exported symbol -> (restype, argtypes); mirrors include/mmsbm.h
 _c_int, _c_i32, _c_i64, _c_dbl, _vp = ctypes.c_int, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 SIGNATURES = {
     "mmsbm_version": (_c_int, []),
-    "mmsbm_tile": (_c_int, []),
+    "mmsbm_chunk": (_c_int, []),
     "mmsbm_last_error": (ctypes.c_char_p, []),
     "mmsbm_create": (_c_int, [_c_int, ctypes.POINTER(_vp)]),
     "mmsbm_destroy": (_c_int, [_vp]),
     "mmsbm_set_shape": (_c_int, [_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_dbl]),
-    "mmsbm_set_links": (_c_int, [_vp, _c_i32, _vp, _c_i64, ctypes.POINTER(_c_i64)]),
-    "mmsbm_set_genes": (_c_int, [_vp, _vp, _vp, _c_i64, _vp]),
+    "mmsbm_set_links": (_c_int, [_vp, _c_i32, _vp, _vp, _c_i64]),
+    "mmsbm_set_degree": (_c_int, [_vp, _vp]),
     "mmsbm_workspace_bytes": (_c_int, [_vp, ctypes.POINTER(_c_i64)]),
     "mmsbm_set_workspace": (_c_int, [_vp, _vp, _c_i64]),
     "mmsbm_iterate": (_c_int, [_vp, _vp, _vp, _c_i32, _vp]),
@@ -41,10 +43,10 @@ SIGNATURES = {
     "mmsbm_predict": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _vp, _vp]),
     "mmsbm_accumulate": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "mmsbm_mstep": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
-    "mmsbm_fused": (_c_int, [_vp, ctypes.POINTER(_c_i32)]),
+    "mmsbm_plan_info": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i64)]),
     "mmsbm_timing": (_c_int, [_vp, _c_i32]),
-    "mmsbm_time_estep": (_c_int, [_vp, _vp, _vp, _c_i32, _vp, ctypes.POINTER(_c_dbl)]),
     "mmsbm_timing_result": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_i64)]),
+    "mmsbm_time_kernel": (_c_int, [_vp, _c_i32, _vp, _vp, _c_i32, _vp, ctypes.POINTER(_c_dbl)]),
 }
 
 _lib = None

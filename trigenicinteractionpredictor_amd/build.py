@@ -37,7 +37,7 @@ def needs_build(out: str = LIB) -> bool:
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    deps = [SRC, os.path.join(INCLUDE, "mmsbm.h")]
+    deps = [SRC, os.path.join(PKG, "csrc", "plan.h"), os.path.join(INCLUDE, "mmsbm.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

@@ -1,0 +1,304 @@
+// plan.h — host-side work plan of the pivot-run EM engine (built once per link set).
+//
+// Input: the reference's link table in `links` insertion order (src/TrigenicInteractionPredictor.py
+// :321-423): ids[E][3] in the string-sorted key order (:349-358), counts[E][R] (:360-368).  One
+// OBSERVATION = one (link, rating r) with n = counts[e][r] > 0 (an unobserved rating adds exactly
+// +0.0 in the reference loop, :1002-1012).
+//
+// For every slot s in {0, 1, 2} ("stream" s) and rating r, the observations are ordered by their
+// slot-s gene (the PIVOT; stable, so ties keep link order).  A pivot run is padded to a multiple of
+// CH = 4 rows with zero-weight rows, so every CHUNK of 4 rows has one pivot gene.  Chunks are
+// grouped into UNITS (one wave each: whole runs where they fit, long runs split) and units into
+// WORKGROUPS of NW units.  Inside a unit, every maximal stretch of one pivot gene accumulates into
+// one PARTIAL ROW (K x K doubles of M^s, see mmsbm.hip); partial rows are numbered in stream
+// order, so the partial rows of one (stream, rating, gene) are contiguous.
+//
+// Row record (int4): (i, j, k, w); stream 0: w = n_r (0 on padding rows); streams 1, 2: w = the
+// stream-0 row of the same observation (its c = n / d lives there), padding rows: w = n_rows0 (a
+// slot that always holds 0).
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+namespace mmsbm_plan {
+
+constexpr int CH = 4;   // observations per chunk (one MFMA k-step)
+constexpr int NW = 8;   // waves (units) per workgroup
+
+struct I4 {
+  int x, y, z, w;
+};
+
+struct Plan {
+  int R = 0, P = 0;
+  int streams = 0;                 // 3 (train: EM) or 1 (likelihood only)
+  std::vector<I4> rows;            // all streams, stream-major then rating-major
+  std::vector<int> chunk_prow;     // partial row of each chunk (-1: likelihood-only plan)
+  std::vector<int> chunk_vslot;    // stream 0: the chunk's pivot gene in its workgroup's gene list
+  std::vector<int> wg_units;       // [n_wg][NW + 1] chunk boundaries of the workgroup's units
+  std::vector<int> wg_code;        // [n_wg] stream * 16 + rating
+  std::vector<int> wg_gene;        // [n_wg + 1] offsets into vgenes (stream-0 workgroups)
+  std::vector<int> vgenes;         // pivot genes of each stream-0 workgroup, ascending
+  std::vector<int> prow_ptr;       // [3][R][P + 1] partial rows of (stream, rating, gene)
+  std::vector<int> prow_gene;      // [n_prows]
+  std::vector<int> sp_desc;        // S-partial workgroups: [n_sp][3] (rating, prow begin, end)
+  int sp_lo[8] = {0}, sp_hi[8] = {0};  // S-partial workgroups of each rating
+  int n_wg_a = 0;                  // stream-0 workgroups (the first n_wg_a)
+  int n_wg_b = 0;                  // stream-1/2 workgroups (the next n_wg_b)
+  int n_sp = 0;
+  int gmax = 0;                    // most genes of one stream-0 workgroup
+  long long n_rows0 = 0;           // rows of stream 0 (the c vector)
+  long long n_prows = 0;
+  long long n_obs = 0;             // real observations (one stream)
+};
+
+// Greedy unit packing over the runs of one (stream, rating): a unit takes whole runs while they
+// fit in `lmax` chunks (and, on stream 0, `gcap` genes), a run longer than `lmax` is split.
+// Returns unit boundaries (chunk offsets relative to the stream section).
+inline void pack_units(const std::vector<int>& run_chunks, int lmax, int gcap, std::vector<int>& ub) {
+  ub.clear();
+  ub.push_back(0);
+  int cur = 0, genes = 0, pos = 0;
+  for (int nch : run_chunks) {
+    if (cur > 0 && (cur + nch > lmax || genes + 1 > gcap)) {
+      ub.push_back(pos);
+      cur = 0;
+      genes = 0;
+    }
+    while (nch > 0) {
+      const int take = std::min(nch, lmax - cur);
+      cur += take;
+      pos += take;
+      nch -= take;
+      if (nch > 0) {  // split: the run continues in the next unit
+        ub.push_back(pos);
+        cur = 0;
+        genes = 0;
+      }
+    }
+    genes += 1;
+  }
+  if (cur > 0) ub.push_back(pos);
+}
+
+// Builds the plan.  units_a / units_b: the number of units to aim for in stream 0 and in streams
+// 1 + 2 together (about 8 waves per CU); gcap: most distinct genes per stream-0 workgroup (its
+// V table lives in LDS).
+inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
+                  int units_a, int units_b, int gcap) {
+  Plan pl;
+  pl.R = R;
+  pl.P = P;
+  pl.streams = em ? 3 : 1;
+  // observations of each rating in link order
+  std::vector<std::vector<int>> obs(R);
+  for (long long e = 0; e < E; ++e)
+    for (int r = 0; r < R; ++r)
+      if (counts[e * R + r] > 0) obs[r].push_back((int)e);
+  for (int r = 0; r < R; ++r) pl.n_obs += (long long)obs[r].size();
+
+  // stream-0 row of each observation (e, r): for the c index of streams 1, 2
+  std::vector<std::vector<int>> row0(R);
+  if (em) pl.prow_ptr.assign((size_t)3 * R * (P + 1), 0);
+
+  // chunk counts of every (stream, rating) for the unit length
+  auto sorted_by = [&](int s, int r) {
+    // counting sort by pivot gene (stable)
+    const std::vector<int>& o = obs[r];
+    std::vector<int> cnt(P + 1, 0);
+    for (int e : o) cnt[ids[(size_t)e * 3 + s] + 1]++;
+    for (int g = 0; g < P; ++g) cnt[g + 1] += cnt[g];
+    std::vector<int> out(o.size());
+    for (int e : o) out[cnt[ids[(size_t)e * 3 + s]]++] = e;
+    return out;
+  };
+
+  long long chunks_a = 0, chunks_b = 0;
+  std::vector<std::vector<int>> order((size_t)3 * R);
+  for (int s = 0; s < pl.streams; ++s)
+    for (int r = 0; r < R; ++r) {
+      order[s * R + r] = sorted_by(s, r);
+      const auto& o = order[s * R + r];
+      long long nch = 0;
+      for (size_t q = 0; q < o.size();) {
+        const int g = ids[(size_t)o[q] * 3 + s];
+        size_t q1 = q;
+        while (q1 < o.size() && ids[(size_t)o[q1] * 3 + s] == g) ++q1;
+        nch += (long long)((q1 - q + CH - 1) / CH);
+        q = q1;
+      }
+      (s == 0 ? chunks_a : chunks_b) += nch;
+    }
+  const int lmax_a = (int)std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1));
+  const int lmax_b = (int)std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1));
+
+  std::vector<int> wg_stream;
+  for (int s = 0; s < pl.streams; ++s) {
+    for (int r = 0; r < R; ++r) {
+      const auto& o = order[s * R + r];
+      const long long row_base = (long long)pl.rows.size();
+      const int chunk_base = (int)(row_base / CH);
+      // rows + runs
+      std::vector<int> run_chunks, run_gene;
+      std::vector<int> pos0;  // stream-0 row of each obs of rating r, indexed like obs[r]
+      for (size_t q = 0; q < o.size();) {
+        const int g = ids[(size_t)o[q] * 3 + s];
+        size_t q1 = q;
+        while (q1 < o.size() && ids[(size_t)o[q1] * 3 + s] == g) ++q1;
+        for (size_t t = q; t < q1; ++t) {
+          const int e = o[t];
+          I4 rec{ids[(size_t)e * 3], ids[(size_t)e * 3 + 1], ids[(size_t)e * 3 + 2], 0};
+          if (s == 0) {
+            rec.w = counts[(size_t)e * R + r];
+          } else {
+            rec.w = -1;  // filled below from the stream-0 row map
+          }
+          pl.rows.push_back(rec);
+        }
+        const int n = (int)(q1 - q);
+        const int pad = (CH - n % CH) % CH;
+        for (int t = 0; t < pad; ++t) pl.rows.push_back(I4{g, g, g, s == 0 ? 0 : -2});
+        run_chunks.push_back((n + pad) / CH);
+        run_gene.push_back(g);
+        q = q1;
+      }
+      // units
+      std::vector<int> ub;
+      pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, s == 0 ? gcap : (1 << 30), ub);
+      const int nunits = (int)ub.size() - 1;
+      // chunk -> gene
+      const int nch = ub.empty() ? 0 : ub.back();
+      std::vector<int> cgene(nch);
+      {
+        int c = 0;
+        for (size_t k = 0; k < run_chunks.size(); ++k)
+          for (int t = 0; t < run_chunks[k]; ++t) cgene[c++] = run_gene[k];
+      }
+      // workgroups: NW consecutive units; stream 0 also caps the distinct genes (V table)
+      std::vector<int> wstart;  // unit index where each workgroup starts
+      {
+        int u = 0;
+        while (u < nunits) {
+          wstart.push_back(u);
+          int taken = 0, genes = 0, last = -1;
+          while (u < nunits && taken < NW) {
+            int ug = 0, lg = last;
+            for (int c = ub[u]; c < ub[u + 1]; ++c)
+              if (cgene[c] != lg) {
+                ++ug;
+                lg = cgene[c];
+              }
+            if (s == 0 && taken > 0 && genes + ug > gcap) break;
+            genes += ug;
+            last = lg;
+            ++taken;
+            ++u;
+          }
+        }
+      }
+      for (size_t w = 0; w < wstart.size(); ++w) {
+        const int u0 = wstart[w];
+        const int u1 = w + 1 < wstart.size() ? wstart[w + 1] : nunits;
+        for (int i = 0; i <= NW; ++i) {
+          const int u = std::min(u0 + i, u1);
+          pl.wg_units.push_back(chunk_base + ub[u]);
+        }
+        pl.wg_code.push_back(s * 16 + r);
+        wg_stream.push_back(s);
+        if (s == 0) {
+          pl.wg_gene.push_back((int)pl.vgenes.size());
+          const int first = (int)pl.vgenes.size();
+          for (int c = ub[u0]; c < ub[u1]; ++c)
+            if ((int)pl.vgenes.size() == first || pl.vgenes.back() != cgene[c]) pl.vgenes.push_back(cgene[c]);
+          for (int c = ub[u0]; c < ub[u1]; ++c) {
+            // genes ascend within the stream, so the slot is a lower_bound in this list
+            const auto it = std::lower_bound(pl.vgenes.begin() + first, pl.vgenes.end(), cgene[c]);
+            pl.chunk_vslot.push_back((int)(it - (pl.vgenes.begin() + first)));
+          }
+          pl.gmax = std::max(pl.gmax, (int)pl.vgenes.size() - first);
+        }
+      }
+      if (s != 0) pl.chunk_vslot.resize(pl.chunk_vslot.size() + nch, 0);
+      // partial rows: a new one at every unit start and every gene change inside a unit
+      if (em) {
+        int* ptr = &pl.prow_ptr[((size_t)s * R + r) * (P + 1)];
+        const long long first_prow = pl.n_prows;
+        int u = 0;
+        for (int c = 0; c < nch; ++c) {
+          while (u + 1 < (int)ub.size() && ub[u + 1] <= c) ++u;
+          if (c == ub[u] || cgene[c] != cgene[c - 1]) {
+            pl.prow_gene.push_back(cgene[c]);
+            ++pl.n_prows;
+          }
+          pl.chunk_prow.push_back((int)(pl.n_prows - 1));
+        }
+        // CSR over genes: prows of stream (s, r) ascend by gene
+        std::vector<int> cnt(P + 1, 0);
+        for (long long q = first_prow; q < pl.n_prows; ++q) cnt[pl.prow_gene[q] + 1]++;
+        ptr[0] = (int)first_prow;
+        for (int g = 0; g < P; ++g) ptr[g + 1] = ptr[g] + cnt[g + 1];
+      } else {
+        pl.chunk_prow.resize(pl.chunk_prow.size() + nch, -1);
+      }
+      if (s == 0) {
+        // stream-0 row of every observation of rating r
+        std::vector<int>& m = row0[r];
+        m.assign(E, -1);
+        long long rr = row_base;
+        for (size_t q = 0; q < o.size();) {
+          const int g = ids[(size_t)o[q] * 3];
+          size_t q1 = q;
+          while (q1 < o.size() && ids[(size_t)o[q1] * 3] == g) ++q1;
+          for (size_t t = q; t < q1; ++t) m[o[t]] = (int)(rr++);
+          rr += (CH - (long long)(q1 - q) % CH) % CH;
+          q = q1;
+        }
+        pl.n_rows0 = (long long)pl.rows.size();
+      } else {
+        // c index of every row of this stream section
+        size_t rr = (size_t)row_base;
+        for (size_t q = 0; q < o.size();) {
+          const int g = ids[(size_t)o[q] * 3 + s];
+          size_t q1 = q;
+          while (q1 < o.size() && ids[(size_t)o[q1] * 3 + s] == g) ++q1;
+          for (size_t t = q; t < q1; ++t) pl.rows[rr++].w = row0[r][o[t]];
+          const int pad = (CH - (int)(q1 - q) % CH) % CH;
+          for (int t = 0; t < pad; ++t) pl.rows[rr++].w = -2;
+          q = q1;
+        }
+      }
+    }
+    if (s == 0) pl.n_wg_a = (int)pl.wg_code.size();
+  }
+  pl.n_wg_b = (int)pl.wg_code.size() - pl.n_wg_a;
+  pl.wg_gene.push_back((int)pl.vgenes.size());
+  for (auto& rec : pl.rows)
+    if (rec.w == -2) rec.w = (int)pl.n_rows0;  // padding rows of streams 1, 2: the zero c slot
+  // S-partial workgroups over the stream-0 partial rows of each rating
+  if (em) {
+    for (int r = 0; r < R; ++r) {
+      const int q0 = pl.prow_ptr[(size_t)r * (P + 1)];
+      const int q1 = pl.prow_ptr[(size_t)r * (P + 1) + P];
+      pl.sp_lo[r] = pl.n_sp;
+      const int n = q1 - q0;
+      const int parts = n <= 0 ? 0 : std::min(64, std::max(1, n / 128));
+      for (int k = 0; k < parts; ++k) {
+        pl.sp_desc.push_back(r);
+        pl.sp_desc.push_back(q0 + (int)((long long)n * k / parts));
+        pl.sp_desc.push_back(q0 + (int)((long long)n * (k + 1) / parts));
+        ++pl.n_sp;
+      }
+      pl.sp_hi[r] = pl.n_sp;
+    }
+    if (pl.n_sp == 0) {  // no observation at all: one empty S workgroup still snapshots p
+      pl.sp_desc.insert(pl.sp_desc.end(), {0, 0, 0});
+      pl.n_sp = 1;
+      pl.sp_hi[0] = 1;
+    }
+  }
+  return pl;
+}
+
+}  // namespace mmsbm_plan
