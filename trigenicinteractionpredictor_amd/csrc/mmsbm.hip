@@ -97,12 +97,10 @@ struct KT {
   // S partials: (a-tile, group of 4 cell tiles) items over the 8 waves
   static constexpr int NCT = (K2 + 3) / 4;
   static constexpr int NCG = (NCT + 3) / 4;
-  static constexpr int NSI = (NG * NCG + NW - 1) / NW;
-  // fin_kernel: genes per workgroup (one thread per (gene, x)), summed M rows in LDS
-  static constexpr int GF = FIN_NT / K;
-  static constexpr int LDS_F = GF * K2 * 8;
+  static constexpr int NSI_ALL = (NG * NCG + NW - 1) / NW;
+  static constexpr int NSI = NSI_ALL < 8 ? NSI_ALL : 8;           // accumulators per wave
+  static constexpr int NIG = (NG * NCG + NW * NSI - 1) / (NW * NSI);  // item groups (workgroups)
   static_assert(LDS_A <= 160 * 1024, "pass A LDS over budget");
-  static_assert(LDS_F <= 64 * 1024, "fin LDS over budget");
 };
 
 int gmax_for(int K);  // host view of KT<K>::GMAX (table below)
@@ -127,13 +125,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 enum { PASS_A = 0, PASS_LL = 1, PASS_B = 2 };
 
-// Gene of observation o (0..3) of a chunk in slot u (sl = 0) or v (sl = 1) of stream s.
-__device__ __forceinline__ int chunk_gene(const int4 (&rec)[CH], int o, int sl, int s) {
-  const int4 e = o == 0 ? rec[0] : o == 1 ? rec[1] : o == 2 ? rec[2] : rec[3];
-  if (sl == 0) return s == 0 ? e.y : e.x;   // u = j (stream 0), else i
-  return s == 2 ? e.y : e.z;                // v = j (stream 2), else k
-}
-
 // ------------------------------------------------------------------------------------------
 // S partial of one workgroup (launch B): S_r[a][cell] += th_g(q)[a] M_q[cell] over the partial rows
 // q of stream 0, rating r, in [q0, q1), cells (b, h) dense.  MFMA k index = four partial rows,
@@ -142,7 +133,8 @@ __device__ __forceinline__ int chunk_gene(const int4 (&rec)[CH], int o, int sl, 
 template <int K>
 __device__ __forceinline__ void s_partial(const double* __restrict__ th, const double* __restrict__ prows_b,
                                           const int* __restrict__ prow_gene, int q0, int q1,
-                                          double* __restrict__ out, int wv, int hi, int blk, int lo) {
+                                          double* __restrict__ out, int ig, int wv, int hi, int blk,
+                                          int lo) {
   using T = KT<K>;
   double acc[T::NSI];
 #pragma unroll
@@ -154,7 +146,7 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
     const double* __restrict__ Mq = prows_b + (size_t)(vq ? qi : q0) * T::K2;
 #pragma unroll
     for (int k = 0; k < T::NSI; ++k) {
-      const int it = wv + NW * k;
+      const int it = ig * NW * T::NSI + wv + NW * k;
       if (it < T::NG * T::NCG) {
         const int at = it / T::NCG, cg = it % T::NCG;
         const int a = 4 * at + lo, cell = 4 * (4 * cg + blk) + lo;
@@ -166,7 +158,7 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
   }
 #pragma unroll
   for (int k = 0; k < T::NSI; ++k) {
-    const int it = wv + NW * k;
+    const int it = ig * NW * T::NSI + wv + NW * k;
     if (it < T::NG * T::NCG) {
       const int at = it / T::NCG, cg = it % T::NCG;
       const int a = 4 * at + hi, cell = 4 * (4 * cg + blk) + lo;
@@ -205,12 +197,12 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 
   if constexpr (MODE == PASS_B) {
     if (w >= n_wg) {  // S partial + snapshot of p for fin_kernel (which updates p in place)
-      const int sp = w - n_wg;
+      const int sw = w - n_wg, sp = sw / T::NIG, ig = sw % T::NIG;
       const int* d = sp_desc + 3 * sp;
       s_partial<K>(th, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
-                   spart + ((size_t)b * n_sp + sp) * T::K3, wv, hi, blk, lo);
-      const long long tot = (long long)R * T::K3;
-      const long long c0 = tot * sp / n_sp, c1 = tot * (sp + 1) / n_sp;
+                   spart + ((size_t)b * n_sp + sp) * T::K3, ig, wv, hi, blk, lo);
+      const long long tot = (long long)R * T::K3, nsw = (long long)n_sp * T::NIG;
+      const long long c0 = tot * sw / nsw, c1 = tot * (sw + 1) / nsw;
       for (long long idx = c0 + tid; idx < c1; idx += NT)
         pold[(size_t)b * tot + idx] = pr[(size_t)b * tot + idx];
       return;
@@ -258,16 +250,18 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
   double* __restrict__ cb = cbuf + (size_t)b * (n_rows0 + 1);
   double* __restrict__ pb = prows + (size_t)b * n_prows * T::K2;
-
-  // staged theta values of one chunk: piece t of lane = (row8 = (64 t + lane) / KP, col)
-  auto stage_load = [&](const int4 (&rec)[CH], double (&v)[T::NPC]) {
+  const int* __restrict__ rows_i = reinterpret_cast<const int*>(rows);
+  // record components: lane l holds int (l & 15) of the chunk's 4 records (i, j, k, w) and the
+  // others read it with a lane shuffle: no register array is indexed at run time
+  const int ucomp = s == 0 ? 1 : 0, vcomp = s == 2 ? 1 : 2;
+  auto ld_rec = [&](int q) { return rows_i[(size_t)q * 16 + (lane & 15)]; };
+  auto stage_load = [&](int rv, double (&v)[T::NPC]) {
 #pragma unroll
     for (int t = 0; t < T::NPC; ++t) {
       const int pc = 64 * t + lane;
-      const int row8 = pc / T::KP, col = pc % T::KP;
-      const bool ok = pc < 8 * T::KP && col < K;
-      const int g = chunk_gene(rec, row8 & 3, (row8 >> 2) & 1, s);
-      v[t] = ok ? th[(size_t)g * K + col] : 0.0;
+      const int row8 = pc < 8 * T::KP ? pc / T::KP : 0, col = pc % T::KP;
+      const int g = __shfl(rv, (row8 & 3) * 4 + ((row8 >> 2) ? vcomp : ucomp), 64);
+      v[t] = (pc < 8 * T::KP && col < K) ? th[(size_t)g * K + col] : 0.0;
     }
   };
   auto stage_store = [&](double* I, const double (&v)[T::NPC]) {
@@ -276,11 +270,6 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       const int pc = 64 * t + lane;
       if (pc < 8 * T::KP) I[(pc / T::KP) * TR + pc % T::KP] = v[t];
     }
-  };
-  auto load_rec = [&](int q, int4 (&rec)[CH]) {
-    const int4* rp = rows + (size_t)q * CH;
-#pragma unroll
-    for (int o = 0; o < CH; ++o) rec[o] = rp[o];
   };
 
   double macc[T::NTS];
@@ -292,27 +281,40 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   wave_lds_sync();
 
   if (c0 < c1) {
-    int4 rec0[CH], rec1[CH], rec2[CH];
-    load_rec(c0, rec0);
-    load_rec(c0 + 1 < c1 ? c0 + 1 : c0, rec1);
+    // pipeline: records + metadata two chunks ahead, theta values (and c) one chunk ahead
+    const int qa = c0 + 1 < c1 ? c0 + 1 : c0;
+    int rv0 = ld_rec(c0), rv1 = ld_rec(qa);
+    int pr0 = 0, pr1 = 0, vs0 = 0, vs1 = 0;
+    if constexpr (MODE != PASS_LL) {
+      pr0 = chunk_prow[c0];
+      pr1 = chunk_prow[qa];
+    }
+    if constexpr (MODE != PASS_B) {
+      vs0 = chunk_vslot[c0];
+      vs1 = chunk_vslot[qa];
+    }
     double stg[T::NPC];
-    stage_load(rec0, stg);
+    stage_load(rv0, stg);
     stage_store(img, stg);
+    double cq = 0.0, cn = 0.0;  // PASS_B: c of this chunk's observation hi, of the next chunk's
+    if constexpr (MODE == PASS_B) cq = cb[__shfl(rv0, hi * 4 + 3, 64)];
     for (int q = c0; q < c1; ++q) {
       const int buf = (q - c0) & 1;
-      // prefetch: records two chunks ahead, theta values of the next chunk
-      load_rec(q + 2 < c1 ? q + 2 : q, rec2);
-      stage_load(rec1, stg);
+      const int qb = q + 2 < c1 ? q + 2 : q;
+      const int rv2 = ld_rec(qb);
+      int pr2 = 0, vs2 = 0;
+      if constexpr (MODE != PASS_LL) pr2 = chunk_prow[qb];
+      if constexpr (MODE != PASS_B) vs2 = chunk_vslot[qb];
+      stage_load(rv1, stg);
+      if constexpr (MODE == PASS_B) cn = cb[__shfl(rv1, hi * 4 + 3, 64)];
       wave_lds_sync();
       const double* I = img + buf * T::IMG;
-      const int4 eh = hi == 0 ? rec0[0] : hi == 1 ? rec0[1] : hi == 2 ? rec0[2] : rec0[3];
 
-      double c;
-      if constexpr (MODE == PASS_B) {
-        c = cb[eh.w];
-      } else {
+      double c = cq;
+      if constexpr (MODE != PASS_B) {
         // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
-        const double* __restrict__ V = Vt + chunk_vslot[q] * T::VDBL;
+        const int nw = __shfl(rv0, hi * 4 + 3, 64);
+        const double* __restrict__ V = Vt + vs0 * T::VDBL;
         double dp = 0.0;
 #pragma unroll
         for (int bg = 0; bg < T::NBG; ++bg) {
@@ -328,9 +330,9 @@ __global__ __launch_bounds__(NT) void pass_kernel(
         dp += __shfl_xor(dp, 8, 64);
         const double d = dp + eps;
         if constexpr (MODE == PASS_LL) {
-          if ((lane & 15) == 0) ll += (double)eh.w * log(d);
+          if ((lane & 15) == 0) ll += (double)nw * log(d);
         } else {
-          c = (double)eh.w / d;
+          c = (double)nw / d;
           if ((lane & 15) == 0) cb[(size_t)q * CH + hi] = c;
         }
       }
@@ -344,10 +346,8 @@ __global__ __launch_bounds__(NT) void pass_kernel(
           const double av = tv ? c * I[hi * TR + 4 * xs + lo] : 0.0;
           macc[ts] = mfma4(av, I[(4 + hi) * TR + 4 * ys + lo], macc[ts]);
         }
-        const int prow = chunk_prow[q];
-        const int nxt = q + 1 < c1 ? chunk_prow[q + 1] : -1;
-        if (nxt != prow) {  // end of this gene stretch: its partial row
-          double* __restrict__ out = pb + (size_t)prow * T::K2;
+        if (q + 1 >= c1 || pr1 != pr0) {  // end of this gene stretch: its partial row
+          double* __restrict__ out = pb + (size_t)pr0 * T::K2;
 #pragma unroll
           for (int ts = 0; ts < T::NTS; ++ts) {
             const int t = 4 * ts + blk;
@@ -360,11 +360,13 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       // next chunk's image into the other buffer (its reads of this buffer are done)
       wave_lds_sync();
       stage_store(img + (buf ^ 1) * T::IMG, stg);
-#pragma unroll
-      for (int o = 0; o < CH; ++o) {
-        rec0[o] = rec1[o];
-        rec1[o] = rec2[o];
-      }
+      rv0 = rv1;
+      rv1 = rv2;
+      pr0 = pr1;
+      pr1 = pr2;
+      vs0 = vs1;
+      vs1 = vs2;
+      cq = cn;
     }
   }
   if constexpr (MODE == PASS_LL) {
@@ -383,15 +385,29 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// fin_kernel, grid (gene workgroups + cell workgroups, B), block 256.
-//   gene part: GF genes, thread (gene, x): X = sum over the three streams and R ratings of the
-//     p-contraction of the gene's summed partial rows (summed in LDS in partial-row order), then
-//     theta' = theta X / deg (SUMS: nth = X, theta untouched).  p is read from the snapshot pold.
+// fin_kernel, grid (gene workgroups + cell workgroups, B), block 256 = 4 waves.
+//   gene part (4 genes = one MFMA row tile per workgroup): for every (stream s, rating r) the
+//     genes' partial rows are summed into LDS (fixed order), then
+//       X[g][x] += sum_k M_{s,r,g}[k] P^s_r[k][x]   (k = the two other axes, dense)
+//     on FP64 MFMA: blocks = x tiles, wave w takes the (combo, x group) items w, w + 4, ...; the
+//     four waves' partial X are summed in LDS in wave order.  theta' = theta X / deg (SUMS: nth).
+//     p is read from the snapshot pold (the cell part below rewrites pr in the same launch).
 //   cell part: S_r = sum of the rating's S partials (fixed order); npr = p S;
 //     p' = npr / (eps + sum_r npr)  (SUMS: S_out = S, p untouched).
 // ------------------------------------------------------------------------------------------
 struct SpRange {
   int lo[MAX_R], hi[MAX_R];
+};
+
+template <int K>
+struct FT {
+  static constexpr int K2 = K * K, NG = (K + 3) / 4;
+  static constexpr int KS = (K2 + 3) / 4;       // k-steps over the dense (y, z) cells
+  static constexpr int K2P = 4 * KS;
+  static constexpr int NXG = (NG + 3) / 4;      // MFMA groups of 4 x tiles
+  static constexpr int CB_RAW = (60 * 1024) / (4 * K2P * 8);
+  static constexpr int CB = CB_RAW > 6 ? 6 : (CB_RAW < 1 ? 1 : CB_RAW);  // combos staged at once
+  static constexpr int LDS = CB * 4 * K2P * 8 > 4 * NXG * 64 * 8 ? CB * 4 * K2P * 8 : 4 * NXG * 64 * 8;
 };
 
 template <int K, bool SUMS>
@@ -401,49 +417,73 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
     const double* __restrict__ spart, const int* __restrict__ deg, SpRange spr, int P, int R,
     long long n_prows, int n_sp, int n_gene_wg, double eps, double* __restrict__ nth_out,
     double* __restrict__ S_out) {
-  using T = KT<K>;
-  constexpr int K2 = T::K2, K3 = T::K3;
-  extern __shared__ __attribute__((aligned(16))) double Ms[];  // [GF][K2]
+  using F = FT<K>;
+  constexpr int K2 = F::K2, K3 = K * K * K, NG = F::NG;
+  extern __shared__ __attribute__((aligned(16))) double Ms[];  // [CB][4 genes][K2P]
   const int tid = threadIdx.x, b = blockIdx.y;
   if ((int)blockIdx.x < n_gene_wg) {
-    const int g0 = blockIdx.x * T::GF;
-    const int gl = tid / K, x = tid % K;
-    const int g = g0 + gl;
-    const bool mine = gl < T::GF && g < P;
-    double X = 0.0;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
+    const int g0 = blockIdx.x * 4;
     const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
-    for (int s = 0; s < 3; ++s) {
-      for (int r = 0; r < R; ++r) {
-        const int* ptr = prow_ptr + ((size_t)s * R + r) * (P + 1);
-        __syncthreads();
-        for (int idx = tid; idx < T::GF * K2; idx += FIN_NT) {
-          const int gg = g0 + idx / K2, cell = idx % K2;
-          double m = 0.0;
-          if (gg < P)
-            for (int q = ptr[gg]; q < ptr[gg + 1]; ++q) m += pb[(size_t)q * K2 + cell];
-          Ms[idx] = m;
+    const int NC = 3 * R;
+    double acc[F::NXG];
+#pragma unroll
+    for (int xg = 0; xg < F::NXG; ++xg) acc[xg] = 0.0;
+    for (int cb0 = 0; cb0 < NC; cb0 += F::CB) {
+      const int ncb = NC - cb0 < F::CB ? NC - cb0 : F::CB;
+      __syncthreads();
+      for (int idx = tid; idx < ncb * 4 * F::K2P; idx += FIN_NT) {
+        const int c = idx / (4 * F::K2P), rem = idx % (4 * F::K2P);
+        const int gl = rem / F::K2P, k = rem % F::K2P;
+        const int g = g0 + gl;
+        double m = 0.0;
+        if (g < P && k < K2) {
+          const int* ptr = prow_ptr + (size_t)(cb0 + c) * (P + 1);  // combo = s * R + r
+          for (int q = ptr[g]; q < ptr[g + 1]; ++q) m += pb[(size_t)q * K2 + k];
         }
-        __syncthreads();
-        if (mine) {
-          const double* __restrict__ M = Ms + gl * K2;
-          const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
-          double acc = 0.0;
-          if (s == 0) {        // X0[a] = sum_bh p[a][b][h] M[b][h]
-            for (int yz = 0; yz < K2; ++yz) acc = fma(p[x * K2 + yz], M[yz], acc);
-          } else if (s == 1) { // X1[b] = sum_ah p[a][b][h] M[a][h]
-            for (int y = 0; y < K; ++y)
-              for (int z = 0; z < K; ++z) acc = fma(p[(y * K + x) * K + z], M[y * K + z], acc);
-          } else {             // X2[h] = sum_ab p[a][b][h] M[a][b]
-            for (int yz = 0; yz < K2; ++yz) acc = fma(p[yz * K + x], M[yz], acc);
+        Ms[idx] = m;
+      }
+      __syncthreads();
+      for (int item = wv; item < ncb * F::NXG; item += 4) {
+        const int c = item / F::NXG, xg = item % F::NXG;
+        const int combo = cb0 + c, s = combo / R, r = combo % R;
+        const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
+        const int x = 4 * (4 * xg + blk) + lo;
+        const double* __restrict__ Mg = Ms + ((size_t)c * 4 + lo) * F::K2P;
+        double a2 = 0.0;
+        for (int ks = 0; ks < F::KS; ++ks) {
+          const int k = 4 * ks + hi;
+          double bv = 0.0;
+          if (k < K2 && x < K) {
+            const int y = k / K, z = k % K;
+            bv = s == 0 ? p[x * K2 + k] : s == 1 ? p[(y * K + x) * K + z] : p[k * K + x];
           }
-          X += acc;
+          a2 = mfma4(Mg[k], bv, a2);
         }
+#pragma unroll
+        for (int q = 0; q < F::NXG; ++q)
+          if (q == xg) acc[q] += a2;
       }
     }
-    if (mine) {
-      const size_t o = ((size_t)b * P + g) * K + x;
-      if constexpr (SUMS) nth_out[o] = X;
-      else theta[o] = theta[o] * X / (double)deg[g];
+    // X[gene hi][x = 4 (4 xg + blk) + lo]: the four waves' partials summed in wave order
+    __syncthreads();
+#pragma unroll
+    for (int xg = 0; xg < F::NXG; ++xg) Ms[(wv * F::NXG + xg) * 64 + lane] = acc[xg];
+    __syncthreads();
+    if (wv == 0) {
+      const int g = g0 + hi;
+#pragma unroll
+      for (int xg = 0; xg < F::NXG; ++xg) {
+        const int x = 4 * (4 * xg + blk) + lo;
+        double X = 0.0;
+        for (int w = 0; w < 4; ++w) X += Ms[(w * F::NXG + xg) * 64 + lane];
+        if (g < P && x < K) {
+          const size_t o = ((size_t)b * P + g) * K + x;
+          if constexpr (SUMS) nth_out[o] = X;
+          else theta[o] = theta[o] * X / (double)deg[g];
+        }
+      }
     }
   } else {
     const int cell = (blockIdx.x - n_gene_wg) * FIN_NT + tid;
@@ -669,7 +709,7 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
   const SetDev& sd = c->sets[which];
   const auto& h = sd.h;
   if (mode == PASS_B) {
-    const int n = h.n_wg_b + h.n_sp;
+    const int n = h.n_wg_b + h.n_sp * T::NIG;
     if (n == 0) return MMSBM_OK;
     pass_kernel<K, PASS_B><<<dim3(n, c->B), NT, T::LDS_B, s>>>(
         sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.wg_units + (size_t)h.n_wg_a * (NW + 1),
@@ -703,19 +743,22 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   using T = KT<K>;
   const SetDev& sd = c->sets[MMSBM_SET_TRAIN];
   const auto& h = sd.h;
-  const int ngw = (c->P + T::GF - 1) / T::GF;
+  const int ngw = (c->P + 3) / 4;
   const int ncw = (T::K3 + FIN_NT - 1) / FIN_NT;
+  int rc;
+  if ((rc = lds_opt_in(c, sums ? 3 : 2, sums ? &fin_kernel<K, true> : &fin_kernel<K, false>, FT<K>::LDS)))
+    return rc;
   SpRange spr{};
   for (int r = 0; r < c->R; ++r) {
     spr.lo[r] = h.sp_lo[r];
     spr.hi[r] = h.sp_hi[r];
   }
   if (sums)
-    fin_kernel<K, true><<<dim3(ngw + ncw, c->B), FIN_NT, T::LDS_F, s>>>(
+    fin_kernel<K, true><<<dim3(ngw + ncw, c->B), FIN_NT, FT<K>::LDS, s>>>(
         theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_sp, 1), ngw, c->eps, nth, S);
   else
-    fin_kernel<K, false><<<dim3(ngw + ncw, c->B), FIN_NT, T::LDS_F, s>>>(
+    fin_kernel<K, false><<<dim3(ngw + ncw, c->B), FIN_NT, FT<K>::LDS, s>>>(
         theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_sp, 1), ngw, c->eps, nth, S);
   HIP_TRY(hipGetLastError());
