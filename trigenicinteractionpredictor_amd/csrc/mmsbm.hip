@@ -139,6 +139,7 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
   double acc[T::NSI];
 #pragma unroll
   for (int k = 0; k < T::NSI; ++k) acc[k] = 0.0;
+#pragma unroll 4
   for (int q = q0; q < q1; q += 4) {
     const int qi = q + hi;
     const bool vq = qi < q1;
@@ -281,32 +282,46 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   wave_lds_sync();
 
   if (c0 < c1) {
-    // pipeline: records + metadata two chunks ahead, theta values (and c) one chunk ahead
-    const int qa = c0 + 1 < c1 ? c0 + 1 : c0;
-    int rv0 = ld_rec(c0), rv1 = ld_rec(qa);
-    int pr0 = 0, pr1 = 0, vs0 = 0, vs1 = 0;
+    // Software pipeline, deep enough to cover an L2 / MALL round trip with a few chunks of work:
+    // records + metadata four chunks ahead, theta values (and c) three ahead, the LDS image of
+    // the next chunk written at the end of this one (double buffer).
+    auto clampq = [&](int q) { return q < c1 ? q : c1 - 1; };
+    int rv0 = ld_rec(c0), rv1 = ld_rec(clampq(c0 + 1)), rv2 = ld_rec(clampq(c0 + 2)),
+        rv3 = ld_rec(clampq(c0 + 3));
+    int pr0 = 0, pr1 = 0, pr2 = 0, pr3 = 0, vs0 = 0, vs1 = 0, vs2 = 0, vs3 = 0;
     if constexpr (MODE != PASS_LL) {
       pr0 = chunk_prow[c0];
-      pr1 = chunk_prow[qa];
+      pr1 = chunk_prow[clampq(c0 + 1)];
+      pr2 = chunk_prow[clampq(c0 + 2)];
+      pr3 = chunk_prow[clampq(c0 + 3)];
     }
     if constexpr (MODE != PASS_B) {
       vs0 = chunk_vslot[c0];
-      vs1 = chunk_vslot[qa];
+      vs1 = chunk_vslot[clampq(c0 + 1)];
+      vs2 = chunk_vslot[clampq(c0 + 2)];
+      vs3 = chunk_vslot[clampq(c0 + 3)];
     }
-    double stg[T::NPC];
-    stage_load(rv0, stg);
-    stage_store(img, stg);
-    double cq = 0.0, cn = 0.0;  // PASS_B: c of this chunk's observation hi, of the next chunk's
-    if constexpr (MODE == PASS_B) cq = cb[__shfl(rv0, hi * 4 + 3, 64)];
+    double st0[T::NPC], st1[T::NPC], st2[T::NPC];  // theta values of chunks q + 1, q + 2, q + 3
+    stage_load(rv0, st0);
+    stage_store(img, st0);
+    stage_load(rv1, st0);
+    stage_load(rv2, st1);
+    // PASS_B: c of observation hi of chunks q .. q + 3
+    double cq = 0.0, cn1 = 0.0, cn2 = 0.0, cn3 = 0.0;
+    if constexpr (MODE == PASS_B) {
+      cq = cb[__shfl(rv0, hi * 4 + 3, 64)];
+      cn1 = cb[__shfl(rv1, hi * 4 + 3, 64)];
+      cn2 = cb[__shfl(rv2, hi * 4 + 3, 64)];
+    }
     for (int q = c0; q < c1; ++q) {
       const int buf = (q - c0) & 1;
-      const int qb = q + 2 < c1 ? q + 2 : q;
-      const int rv2 = ld_rec(qb);
-      int pr2 = 0, vs2 = 0;
-      if constexpr (MODE != PASS_LL) pr2 = chunk_prow[qb];
-      if constexpr (MODE != PASS_B) vs2 = chunk_vslot[qb];
-      stage_load(rv1, stg);
-      if constexpr (MODE == PASS_B) cn = cb[__shfl(rv1, hi * 4 + 3, 64)];
+      const int qb = clampq(q + 4);
+      const int rv4 = ld_rec(qb);
+      int pr4 = 0, vs4 = 0;
+      if constexpr (MODE != PASS_LL) pr4 = chunk_prow[qb];
+      if constexpr (MODE != PASS_B) vs4 = chunk_vslot[qb];
+      stage_load(rv3, st2);
+      if constexpr (MODE == PASS_B) cn3 = cb[__shfl(rv3, hi * 4 + 3, 64)];
       wave_lds_sync();
       const double* I = img + buf * T::IMG;
 
@@ -359,14 +374,27 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       }
       // next chunk's image into the other buffer (its reads of this buffer are done)
       wave_lds_sync();
-      stage_store(img + (buf ^ 1) * T::IMG, stg);
+      stage_store(img + (buf ^ 1) * T::IMG, st0);
+#pragma unroll
+      for (int t = 0; t < T::NPC; ++t) {
+        st0[t] = st1[t];
+        st1[t] = st2[t];
+      }
       rv0 = rv1;
       rv1 = rv2;
+      rv2 = rv3;
+      rv3 = rv4;
       pr0 = pr1;
       pr1 = pr2;
+      pr2 = pr3;
+      pr3 = pr4;
       vs0 = vs1;
       vs1 = vs2;
-      cq = cn;
+      vs2 = vs3;
+      vs3 = vs4;
+      cq = cn1;
+      cn1 = cn2;
+      cn2 = cn3;
     }
   }
   if constexpr (MODE == PASS_LL) {
@@ -451,15 +479,28 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
         const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
         const int x = 4 * (4 * xg + blk) + lo;
         const double* __restrict__ Mg = Ms + ((size_t)c * 4 + lo) * F::K2P;
+        // B operand P^s[k][x]: s = 0 p[x][y][z] = p[x K2 + k], s = 2 p[y][z][x] = p[k K + x],
+        // s = 1 p[y][x][z] (k = y K + z).  Four k-steps per round: their loads go out together.
+        auto pidx = [&](int k) {
+          if (s == 0) return x * K2 + k;
+          if (s == 2) return k * K + x;
+          const int y = k / K;
+          return (y * K + x) * K + (k - y * K);
+        };
+        const bool xv = x < K;
         double a2 = 0.0;
-        for (int ks = 0; ks < F::KS; ++ks) {
-          const int k = 4 * ks + hi;
-          double bv = 0.0;
-          if (k < K2 && x < K) {
-            const int y = k / K, z = k % K;
-            bv = s == 0 ? p[x * K2 + k] : s == 1 ? p[(y * K + x) * K + z] : p[k * K + x];
+#pragma unroll 1
+        for (int ks = 0; ks < F::KS; ks += 4) {
+          double av[4], bv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int k = 4 * (ks + u) + hi;
+            const bool ok = ks + u < F::KS;
+            av[u] = ok ? Mg[k] : 0.0;
+            bv[u] = (ok && xv && k < K2) ? p[pidx(k)] : 0.0;
           }
-          a2 = mfma4(Mg[k], bv, a2);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) a2 = mfma4(av[u], bv[u], a2);
         }
 #pragma unroll
         for (int q = 0; q < F::NXG; ++q)
