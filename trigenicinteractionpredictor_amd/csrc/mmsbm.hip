@@ -90,9 +90,9 @@ struct KT {
   static constexpr int IMG = 8 * TR;              // one chunk: th_u rows of obs 0-3, th_v rows
   static constexpr int NPC = (8 * KP + 63) / 64;  // staged doubles per lane per chunk
   static constexpr int IMG_BYTES = NW * 2 * IMG * 8;
-  static constexpr int GMAX_RAW = (lds_target(K) - IMG_BYTES - 64) / (VDBL * 8);
+  static constexpr int GMAX_RAW = (lds_target(K) - IMG_BYTES - 64) / ((VDBL + KP) * 8);
   static constexpr int GMAX = GMAX_RAW > 64 ? 64 : (GMAX_RAW < 4 ? 4 : GMAX_RAW);
-  static constexpr int LDS_A = GMAX * VDBL * 8 + IMG_BYTES + 64;
+  static constexpr int LDS_A = GMAX * VDBL * 8 + GMAX * KP * 8 + IMG_BYTES + 64;
   static constexpr int LDS_B = IMG_BYTES + 64;
   // S partials: (a-tile, group of 4 cell tiles) items over the 8 waves
   static constexpr int NCT = (K2 + 3) / 4;
@@ -214,7 +214,35 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   const int s = code >> 4, r = code & 15;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * T::K3;
   double* Vt = smem;
-  double* img = smem + (MODE == PASS_B ? 0 : T::GMAX * T::VDBL) + wv * 2 * T::IMG;
+  double* Tg = smem + (MODE == PASS_B ? 0 : T::GMAX * T::VDBL);  // theta rows of the V genes
+  double* img = smem + (MODE == PASS_B ? 0 : T::GMAX * (T::VDBL + T::KP)) + wv * 2 * T::IMG;
+
+  // this wave's unit, and the first records of its pipeline (in flight during the V prologue)
+  const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
+  const int* __restrict__ rows_i = reinterpret_cast<const int*>(rows);
+  auto ld_rec = [&](int q) { return rows_i[(size_t)q * 16 + (lane & 15)]; };
+  auto clampq = [&](int q) { return q < c1 ? q : c1 - 1; };
+  const bool any = c0 < c1;
+  int rv0 = 0, rv1 = 0, rv2 = 0, rv3 = 0;
+  int pr0 = 0, pr1 = 0, pr2 = 0, pr3 = 0, vs0 = 0, vs1 = 0, vs2 = 0, vs3 = 0;
+  if (any) {
+    rv0 = ld_rec(c0);
+    rv1 = ld_rec(clampq(c0 + 1));
+    rv2 = ld_rec(clampq(c0 + 2));
+    rv3 = ld_rec(clampq(c0 + 3));
+    if constexpr (MODE != PASS_LL) {
+      pr0 = chunk_prow[c0];
+      pr1 = chunk_prow[clampq(c0 + 1)];
+      pr2 = chunk_prow[clampq(c0 + 2)];
+      pr3 = chunk_prow[clampq(c0 + 3)];
+    }
+    if constexpr (MODE != PASS_B) {
+      vs0 = chunk_vslot[c0];
+      vs1 = chunk_vslot[clampq(c0 + 1)];
+      vs2 = chunk_vslot[clampq(c0 + 2)];
+      vs3 = chunk_vslot[clampq(c0 + 3)];
+    }
+  }
 
   if constexpr (MODE != PASS_B) {
     // ---- V_g[b][h] = sum_a th_g[a] p_r[a][b][h] for the workgroup's pivot genes (LDS)
@@ -223,39 +251,53 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     if constexpr (ZR > 0)
       for (int idx = tid; idx < ng * ZR; idx += NT)
         Vt[(idx / ZR) * T::VDBL + K * VR + idx % ZR] = 0.0;
+    for (int idx = tid; idx < ((ng + 3) & ~3) * T::KP; idx += NT) {  // theta rows, zero padded
+      const int gl = idx / T::KP, a = idx % T::KP;
+      Tg[idx] = (gl < ng && a < K) ? th[(size_t)vgenes[gb + gl] * K + a] : 0.0;
+    }
+    __syncthreads();
     constexpr int CT = K * NG;  // (b, h tile) cell tiles
     constexpr int CG = (CT + 3) / 4;
     const int GT = (ng + 3) / 4;
-    for (int item = wv; item < GT * CG; item += NW) {
-      const int gt = item / CG, cg = item % CG;
-      const int ct = 4 * cg + blk;
-      const bool cv = ct < CT;
-      const int bb = cv ? ct / NG : 0, hs = cv ? ct % NG : 0;
-      const int gl = 4 * gt + lo;
-      const int gene = vgenes[gb + (gl < ng ? gl : 0)];
-      const int hh = 4 * hs + lo;
-      double acc = 0.0;
+    // items (gene tile, 4 cell tiles); two per round so their p loads go out together
+    for (int i0 = wv; i0 < GT * CG; i0 += 2 * NW) {
+      double av[2][NG], bv[2][NG];
 #pragma unroll
-      for (int as = 0; as < NG; ++as) {
-        const int a = 4 * as + hi;
-        const double av = (gl < ng && a < K) ? th[(size_t)gene * K + a] : 0.0;
-        const double bv = (cv && a < K && hh < K) ? p[(a * K + bb) * K + hh] : 0.0;
-        acc = mfma4(av, bv, acc);
+      for (int u = 0; u < 2; ++u) {
+        const int item = i0 + u * NW;
+        const bool iv = item < GT * CG;
+        const int gt = iv ? item / CG : 0, cg = iv ? item % CG : 0;
+        const int ct = 4 * cg + blk;
+        const bool cv = iv && ct < CT;
+        const int bb = cv ? ct / NG : 0, hh = cv ? 4 * (ct % NG) + lo : 0;
+#pragma unroll
+        for (int as = 0; as < NG; ++as) {
+          const int a = 4 * as + hi;
+          av[u][as] = Tg[(4 * gt + lo) * T::KP + a];
+          bv[u][as] = (cv && a < K && hh < K) ? p[(a * K + bb) * K + hh] : 0.0;
+        }
       }
-      const int go = 4 * gt + hi;
-      if (cv && go < ng) Vt[go * T::VDBL + bb * VR + hh] = acc;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int item = i0 + u * NW;
+        double acc = 0.0;
+#pragma unroll
+        for (int as = 0; as < NG; ++as) acc = mfma4(av[u][as], bv[u][as], acc);
+        const int gt = item / CG, cg = item % CG;
+        const int ct = 4 * cg + blk;
+        const int go = 4 * gt + hi;
+        if (item < GT * CG && ct < CT && go < ng)
+          Vt[go * T::VDBL + (ct / NG) * VR + 4 * (ct % NG) + lo] = acc;
+      }
     }
     __syncthreads();
   }
 
-  const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
   double* __restrict__ cb = cbuf + (size_t)b * (n_rows0 + 1);
   double* __restrict__ pb = prows + (size_t)b * n_prows * T::K2;
-  const int* __restrict__ rows_i = reinterpret_cast<const int*>(rows);
   // record components: lane l holds int (l & 15) of the chunk's 4 records (i, j, k, w) and the
   // others read it with a lane shuffle: no register array is indexed at run time
   const int ucomp = s == 0 ? 1 : 0, vcomp = s == 2 ? 1 : 2;
-  auto ld_rec = [&](int q) { return rows_i[(size_t)q * 16 + (lane & 15)]; };
   auto stage_load = [&](int rv, double (&v)[T::NPC]) {
 #pragma unroll
     for (int t = 0; t < T::NPC; ++t) {
@@ -281,26 +323,10 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   for (int idx = lane; idx < 2 * T::IMG; idx += 64) img[idx] = 0.0;
   wave_lds_sync();
 
-  if (c0 < c1) {
+  if (any) {
     // Software pipeline, deep enough to cover an L2 / MALL round trip with a few chunks of work:
     // records + metadata four chunks ahead, theta values (and c) three ahead, the LDS image of
     // the next chunk written at the end of this one (double buffer).
-    auto clampq = [&](int q) { return q < c1 ? q : c1 - 1; };
-    int rv0 = ld_rec(c0), rv1 = ld_rec(clampq(c0 + 1)), rv2 = ld_rec(clampq(c0 + 2)),
-        rv3 = ld_rec(clampq(c0 + 3));
-    int pr0 = 0, pr1 = 0, pr2 = 0, pr3 = 0, vs0 = 0, vs1 = 0, vs2 = 0, vs3 = 0;
-    if constexpr (MODE != PASS_LL) {
-      pr0 = chunk_prow[c0];
-      pr1 = chunk_prow[clampq(c0 + 1)];
-      pr2 = chunk_prow[clampq(c0 + 2)];
-      pr3 = chunk_prow[clampq(c0 + 3)];
-    }
-    if constexpr (MODE != PASS_B) {
-      vs0 = chunk_vslot[c0];
-      vs1 = chunk_vslot[clampq(c0 + 1)];
-      vs2 = chunk_vslot[clampq(c0 + 2)];
-      vs3 = chunk_vslot[clampq(c0 + 3)];
-    }
     double st0[T::NPC], st1[T::NPC], st2[T::NPC];  // theta values of chunks q + 1, q + 2, q + 3
     stage_load(rv0, st0);
     stage_store(img, st0);
@@ -527,22 +553,41 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
       }
     }
   } else {
-    const int cell = (blockIdx.x - n_gene_wg) * FIN_NT + tid;
-    if (cell >= K3) return;
+    // 64 cells per workgroup, four threads per cell, each summing a quarter of the rating's S
+    // partials (eight loads in flight), the quarters combined in order through LDS
+    const int cl = tid & 63, part = tid >> 6;
+    const int cell = (blockIdx.x - n_gene_wg) * 64 + cl;
+    const bool cv = cell < K3;
     double npr[MAX_R];
     double den = eps;
     for (int r = 0; r < R; ++r) {
+      const int n = spr.hi[r] - spr.lo[r];
+      const int s0 = spr.lo[r] + n * part / 4, s1 = spr.lo[r] + n * (part + 1) / 4;
       double S = 0.0;
-      for (int sp = spr.lo[r]; sp < spr.hi[r]; ++sp) S += spart[((size_t)b * n_sp + sp) * K3 + cell];
-      if constexpr (SUMS) {
-        S_out[((size_t)b * R + r) * K3 + cell] = S;
-      } else {
-        npr[r] = pold[((size_t)b * R + r) * K3 + cell] * S;
-        den += npr[r];
+      for (int sp = s0; sp < s1; sp += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[u] = (cv && sp + u < s1) ? spart[((size_t)b * n_sp + sp + u) * K3 + cell] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) S += v[u];
+      }
+      __syncthreads();
+      Ms[part * 64 + cl] = S;
+      __syncthreads();
+      if (part == 0 && cv) {
+        S = ((Ms[cl] + Ms[64 + cl]) + Ms[128 + cl]) + Ms[192 + cl];
+        if constexpr (SUMS) {
+          S_out[((size_t)b * R + r) * K3 + cell] = S;
+        } else {
+          npr[r] = pold[((size_t)b * R + r) * K3 + cell] * S;
+          den += npr[r];
+        }
       }
     }
     if constexpr (!SUMS)
-      for (int r = 0; r < R; ++r) pr[((size_t)b * R + r) * K3 + cell] = npr[r] / den;
+      if (part == 0 && cv)
+        for (int r = 0; r < R; ++r) pr[((size_t)b * R + r) * K3 + cell] = npr[r] / den;
   }
 }
 
@@ -785,7 +830,7 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   const SetDev& sd = c->sets[MMSBM_SET_TRAIN];
   const auto& h = sd.h;
   const int ngw = (c->P + 3) / 4;
-  const int ncw = (T::K3 + FIN_NT - 1) / FIN_NT;
+  const int ncw = (T::K3 + 63) / 64;
   int rc;
   if ((rc = lds_opt_in(c, sums ? 3 : 2, sums ? &fin_kernel<K, true> : &fin_kernel<K, false>, FT<K>::LDS)))
     return rc;
