@@ -123,6 +123,26 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// v of another lane of the same 16-lane row, by DPP (no LDS round trip): CTRL 0xB1 / 0x4E swap
+// neighbours / pairs of a quad, 0x141 mirrors each half-row, 0x140 mirrors the row.
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const long long x = __double_as_longlong(v);
+  const int l = __builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+  const int h = __builtin_amdgcn_mov_dpp((int)(x >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)h << 32) | (unsigned int)l);
+}
+
+// Sum over the 16 lanes of a row; every lane gets the same bits (each step adds a lane pair
+// that is symmetric under the step's permutation).
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0x140>(v);
+  return v;
+}
+
 enum { PASS_A = 0, PASS_LL = 1, PASS_B = 2 };
 
 // ------------------------------------------------------------------------------------------
@@ -217,32 +237,28 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   double* Tg = smem + (MODE == PASS_B ? 0 : T::GMAX * T::VDBL);  // theta rows of the V genes
   double* img = smem + (MODE == PASS_B ? 0 : T::GMAX * (T::VDBL + T::KP)) + wv * 2 * T::IMG;
 
-  // this wave's unit, and the first records of its pipeline (in flight during the V prologue)
+  // this wave's unit, and the first records of its pipeline (in flight during the V prologue).
+  // Record stream: lane l < 16 holds int l of the chunk's 4 records (i, j, k, w), lane 16 the
+  // chunk's partial row, lane 17 its V slot; the other lanes read them by readlane / shuffle, so
+  // no register array is indexed at run time.
+  constexpr int DR = 6;  // records this many chunks ahead
   const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
   const int* __restrict__ rows_i = reinterpret_cast<const int*>(rows);
-  auto ld_rec = [&](int q) { return rows_i[(size_t)q * 16 + (lane & 15)]; };
+  auto ld_rec = [&](int q) -> int {
+    const int l = lane & 31;
+    if (l < 16) return rows_i[(size_t)q * 16 + l];
+    if constexpr (MODE != PASS_LL)
+      if (l == 16) return chunk_prow[q];
+    if constexpr (MODE != PASS_B)
+      if (l == 17) return chunk_vslot[q];
+    return 0;
+  };
   auto clampq = [&](int q) { return q < c1 ? q : c1 - 1; };
   const bool any = c0 < c1;
-  int rv0 = 0, rv1 = 0, rv2 = 0, rv3 = 0;
-  int pr0 = 0, pr1 = 0, pr2 = 0, pr3 = 0, vs0 = 0, vs1 = 0, vs2 = 0, vs3 = 0;
-  if (any) {
-    rv0 = ld_rec(c0);
-    rv1 = ld_rec(clampq(c0 + 1));
-    rv2 = ld_rec(clampq(c0 + 2));
-    rv3 = ld_rec(clampq(c0 + 3));
-    if constexpr (MODE != PASS_LL) {
-      pr0 = chunk_prow[c0];
-      pr1 = chunk_prow[clampq(c0 + 1)];
-      pr2 = chunk_prow[clampq(c0 + 2)];
-      pr3 = chunk_prow[clampq(c0 + 3)];
-    }
-    if constexpr (MODE != PASS_B) {
-      vs0 = chunk_vslot[c0];
-      vs1 = chunk_vslot[clampq(c0 + 1)];
-      vs2 = chunk_vslot[clampq(c0 + 2)];
-      vs3 = chunk_vslot[clampq(c0 + 3)];
-    }
-  }
+  int rv[DR + 1];
+#pragma unroll
+  for (int i = 0; i < DR; ++i) rv[i] = any ? ld_rec(clampq(c0 + i)) : 0;
+  rv[DR] = 0;
 
   if constexpr (MODE != PASS_B) {
     // ---- V_g[b][h] = sum_a th_g[a] p_r[a][b][h] for the workgroup's pivot genes (LDS)
@@ -323,39 +339,42 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   for (int idx = lane; idx < 2 * T::IMG; idx += 64) img[idx] = 0.0;
   wave_lds_sync();
 
+  // w of observation hi (count on stream 0, c index on streams 1 / 2) of a record register
+  auto rec_w = [&](int r) {
+    const int w0 = __builtin_amdgcn_readlane(r, 3), w1 = __builtin_amdgcn_readlane(r, 7);
+    const int w2 = __builtin_amdgcn_readlane(r, 11), w3 = __builtin_amdgcn_readlane(r, 15);
+    return hi == 0 ? w0 : hi == 1 ? w1 : hi == 2 ? w2 : w3;
+  };
   if (any) {
     // Software pipeline, deep enough to cover an L2 / MALL round trip with a few chunks of work:
-    // records + metadata four chunks ahead, theta values (and c) three ahead, the LDS image of
-    // the next chunk written at the end of this one (double buffer).
-    double st0[T::NPC], st1[T::NPC], st2[T::NPC];  // theta values of chunks q + 1, q + 2, q + 3
-    stage_load(rv0, st0);
-    stage_store(img, st0);
-    stage_load(rv1, st0);
-    stage_load(rv2, st1);
-    // PASS_B: c of observation hi of chunks q .. q + 3
-    double cq = 0.0, cn1 = 0.0, cn2 = 0.0, cn3 = 0.0;
+    // records + metadata DR chunks ahead, theta values (and c) three ahead, the LDS image of the
+    // next chunk written at the end of this one (double buffer).
+    double st[3][T::NPC];  // theta values of chunks q + 1, q + 2, q + 3
+    stage_load(rv[0], st[0]);
+    stage_store(img, st[0]);
+    stage_load(rv[1], st[0]);
+    stage_load(rv[2], st[1]);
+    double cn[4] = {0.0, 0.0, 0.0, 0.0};  // PASS_B: c of observation hi of chunks q .. q + 3
     if constexpr (MODE == PASS_B) {
-      cq = cb[__shfl(rv0, hi * 4 + 3, 64)];
-      cn1 = cb[__shfl(rv1, hi * 4 + 3, 64)];
-      cn2 = cb[__shfl(rv2, hi * 4 + 3, 64)];
+      cn[0] = cb[rec_w(rv[0])];
+      cn[1] = cb[rec_w(rv[1])];
+      cn[2] = cb[rec_w(rv[2])];
     }
     for (int q = c0; q < c1; ++q) {
       const int buf = (q - c0) & 1;
-      const int qb = clampq(q + 4);
-      const int rv4 = ld_rec(qb);
-      int pr4 = 0, vs4 = 0;
-      if constexpr (MODE != PASS_LL) pr4 = chunk_prow[qb];
-      if constexpr (MODE != PASS_B) vs4 = chunk_vslot[qb];
-      stage_load(rv3, st2);
-      if constexpr (MODE == PASS_B) cn3 = cb[__shfl(rv3, hi * 4 + 3, 64)];
+      rv[DR] = ld_rec(clampq(q + DR));
+      stage_load(rv[3], st[2]);
+      if constexpr (MODE == PASS_B) cn[3] = cb[rec_w(rv[3])];
       wave_lds_sync();
       const double* I = img + buf * T::IMG;
+      const int pr0 = __builtin_amdgcn_readlane(rv[0], 16);
+      const int pr1 = __builtin_amdgcn_readlane(rv[1], 16);
 
-      double c = cq;
+      double c = cn[0];
       if constexpr (MODE != PASS_B) {
         // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
-        const int nw = __shfl(rv0, hi * 4 + 3, 64);
-        const double* __restrict__ V = Vt + vs0 * T::VDBL;
+        const int nw = rec_w(rv[0]);
+        const double* __restrict__ V = Vt + __builtin_amdgcn_readlane(rv[0], 17) * T::VDBL;
         double dp = 0.0;
 #pragma unroll
         for (int bg = 0; bg < T::NBG; ++bg) {
@@ -365,11 +384,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
             z = mfma4(I[(4 + lo) * TR + 4 * hs + hi], V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
           dp = fma(I[hi * TR + 16 * bg + 4 * blk + lo], z, dp);
         }
-        dp += __shfl_xor(dp, 1, 64);
-        dp += __shfl_xor(dp, 2, 64);
-        dp += __shfl_xor(dp, 4, 64);
-        dp += __shfl_xor(dp, 8, 64);
-        const double d = dp + eps;
+        const double d = row16_sum(dp) + eps;
         if constexpr (MODE == PASS_LL) {
           if ((lane & 15) == 0) ll += (double)nw * log(d);
         } else {
@@ -400,27 +415,16 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       }
       // next chunk's image into the other buffer (its reads of this buffer are done)
       wave_lds_sync();
-      stage_store(img + (buf ^ 1) * T::IMG, st0);
+      stage_store(img + (buf ^ 1) * T::IMG, st[0]);
 #pragma unroll
       for (int t = 0; t < T::NPC; ++t) {
-        st0[t] = st1[t];
-        st1[t] = st2[t];
+        st[0][t] = st[1][t];
+        st[1][t] = st[2][t];
       }
-      rv0 = rv1;
-      rv1 = rv2;
-      rv2 = rv3;
-      rv3 = rv4;
-      pr0 = pr1;
-      pr1 = pr2;
-      pr2 = pr3;
-      pr3 = pr4;
-      vs0 = vs1;
-      vs1 = vs2;
-      vs2 = vs3;
-      vs3 = vs4;
-      cq = cn1;
-      cn1 = cn2;
-      cn2 = cn3;
+#pragma unroll
+      for (int i = 0; i < DR; ++i) rv[i] = rv[i + 1];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) cn[i] = cn[i + 1];
     }
   }
   if constexpr (MODE == PASS_LL) {
@@ -461,7 +465,9 @@ struct FT {
   static constexpr int NXG = (NG + 3) / 4;      // MFMA groups of 4 x tiles
   static constexpr int CB_RAW = (60 * 1024) / (4 * K2P * 8);
   static constexpr int CB = CB_RAW > 6 ? 6 : (CB_RAW < 1 ? 1 : CB_RAW);  // combos staged at once
-  static constexpr int LDS = CB * 4 * K2P * 8 > 4 * NXG * 64 * 8 ? CB * 4 * K2P * 8 : 4 * NXG * 64 * 8;
+  static constexpr int MS = CB * 4 * K2P > 4 * NXG * 64 ? CB * 4 * K2P : 4 * NXG * 64;  // doubles
+  static constexpr bool PLDS = K <= 12;  // p of every rating staged in LDS (else read from L2)
+  static constexpr int LDS = (MS + (PLDS ? MAX_R * K * K * K : 0)) * 8;
 };
 
 template <int K, bool SUMS>
@@ -481,6 +487,9 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
     const int g0 = blockIdx.x * 4;
     const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
     const int NC = 3 * R;
+    double* Ps = Ms + F::MS;  // [R][K3] when F::PLDS
+    if constexpr (F::PLDS)
+      for (int idx = tid; idx < R * K3; idx += FIN_NT) Ps[idx] = pold[(size_t)b * R * K3 + idx];
     double acc[F::NXG];
 #pragma unroll
     for (int xg = 0; xg < F::NXG; ++xg) acc[xg] = 0.0;
@@ -502,7 +511,7 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
       for (int item = wv; item < ncb * F::NXG; item += 4) {
         const int c = item / F::NXG, xg = item % F::NXG;
         const int combo = cb0 + c, s = combo / R, r = combo % R;
-        const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
+        const double* __restrict__ p = (F::PLDS ? Ps : pold + (size_t)b * R * K3) + (size_t)r * K3;
         const int x = 4 * (4 * xg + blk) + lo;
         const double* __restrict__ Mg = Ms + ((size_t)c * 4 + lo) * F::K2P;
         // B operand P^s[k][x]: s = 0 p[x][y][z] = p[x K2 + k], s = 2 p[y][z][x] = p[k K + x],
@@ -834,17 +843,18 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   int rc;
   if ((rc = lds_opt_in(c, sums ? 3 : 2, sums ? &fin_kernel<K, true> : &fin_kernel<K, false>, FT<K>::LDS)))
     return rc;
+  const int lds = (FT<K>::MS + (FT<K>::PLDS ? c->R * T::K3 : 0)) * 8;  // p staged for R ratings
   SpRange spr{};
   for (int r = 0; r < c->R; ++r) {
     spr.lo[r] = h.sp_lo[r];
     spr.hi[r] = h.sp_hi[r];
   }
   if (sums)
-    fin_kernel<K, true><<<dim3(ngw + ncw, c->B), FIN_NT, FT<K>::LDS, s>>>(
+    fin_kernel<K, true><<<dim3(ngw + ncw, c->B), FIN_NT, lds, s>>>(
         theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_sp, 1), ngw, c->eps, nth, S);
   else
-    fin_kernel<K, false><<<dim3(ngw + ncw, c->B), FIN_NT, FT<K>::LDS, s>>>(
+    fin_kernel<K, false><<<dim3(ngw + ncw, c->B), FIN_NT, lds, s>>>(
         theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_sp, 1), ngw, c->eps, nth, S);
   HIP_TRY(hipGetLastError());
@@ -997,7 +1007,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   const bool em = which == MMSBM_SET_TRAIN;
   // unit counts do not depend on B, so a sample's sums (and its bits) are the same whatever its
   // batch; MMSBM_UNITS="a,b" overrides them (tests: tiny units force every split path)
-  int units_a = 2048, units_b = 4096;
+  int units_a = 3072, units_b = 6144;
   if (const char* u = getenv("MMSBM_UNITS")) {
     int a = 0, b = 0;
     if (sscanf(u, "%d,%d", &a, &b) == 2 && a > 0 && b > 0) {
