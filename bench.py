@@ -289,8 +289,8 @@ def main():
             thetas.append(np.array(host._theta))
             prs.append(np.array(host._pr))
     eng = EMEngine(K, host.P, B=B, device=dev)
-    ids, counts = links_to_arrays(host.links)
-    tids, tcounts = links_to_arrays(host.test_links)
+    ids, counts = host._link_arrays(0)           # the native reader's arrays (links order)
+    tids, tcounts = host._link_arrays(1)
     if links_mode:
         from trigenicinteractionpredictor_amd.linkshard import LinkShardedEM, shard_links
         runner = LinkShardedEM(eng, ids, counts, tids, tcounts)
@@ -355,6 +355,8 @@ def main():
             if rec.get("E_obs") == E_obs and rec.get("B") == B:
                 traffic = rec.get("hbm_bytes_per_launch", {}).get(dom)
         iter_s = elapsed / args.steps
+        wl = ("fold0 stand-in" if (args.P, args.E) == (1500, 90000) else
+              "synthetic P=%d, E=%d" % (host.P, args.E))
         s8d_flops = 8.0 * K ** 3 * E_obs * B      # SURVEY.md 8d's credit for one iteration
         line = {
             "metric": "EM-iterations/sec + final log-likelihood, fold0 K=%d" % K,
@@ -369,10 +371,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic fold0 stand-in (real fold0 is a Git-LFS pointer)",
-            "config": {"workload": ("fold0 stand-in, K=%d, %d sample(s) link-sharded over %d GPU(s)"
-                                    % (K, B, world)) if links_mode else
-                                   "fold0 stand-in, K=%d, %d sample(s)/GPU" % (K, B), "K": K,
-                       "P": host.P, "E_train": len(host.links), "E_test": len(host.test_links),
+            "config": {"workload": ("%s, K=%d, %d sample(s) link-sharded over %d GPU(s)"
+                                    % (wl, K, B, world)) if links_mode else
+                                   "%s, K=%d, %d sample(s)/GPU" % (wl, K, B), "K": K,
+                       "P": host.P, "E_train": int(ids.shape[0]), "E_test": int(tids.shape[0]),
                        "E_obs": E_obs, "samples_per_gpu": B,
                        "parallelism": ("link-sharded x%d" if links_mode else "restart-sharded x%d") % world},
             "world_size": dist.get_world_size() if world > 1 else 1,

@@ -123,6 +123,28 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Measurement builds only (-DMMSBM_STAMP=1, then MMSBM_STAMP=1 at run time): every wave records
+// s_memtime at its phase boundaries; mmsbm_iterate prints per-kernel phase averages.  The
+// product build compiles all of it out.
+#ifndef MMSBM_STAMP
+#define MMSBM_STAMP 0
+#endif
+__device__ unsigned long long* g_stamp = nullptr;
+constexpr int STAMP_SLOTS = 6;
+constexpr long long STAMP_WAVES = 1 << 16;  // per kernel id
+struct Stamp {
+  unsigned long long t[STAMP_SLOTS];
+  __device__ __forceinline__ void mark(int i) {
+    if constexpr (MMSBM_STAMP) t[i] = __builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void flush(int kid, long long wave, int lane) {
+    if constexpr (MMSBM_STAMP) {
+      if (g_stamp && lane == 0 && wave < STAMP_WAVES)
+        for (int i = 0; i < STAMP_SLOTS; ++i) g_stamp[((long long)kid * STAMP_WAVES + wave) * STAMP_SLOTS + i] = t[i];
+    }
+  }
+};
+
 // v of another lane of the same 16-lane row, by DPP (no LDS round trip): CTRL 0xB1 / 0x4E swap
 // neighbours / pairs of a quad, 0x141 mirrors each half-row, 0x140 mirrors the row.
 template <int CTRL>
@@ -215,6 +237,9 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
   const int w = blockIdx.x, b = blockIdx.y;
   const double* __restrict__ th = theta + (size_t)b * P * K;
+  Stamp st_{};
+  st_.mark(0);
+  const long long wave_id = ((long long)b * gridDim.x + w) * NW + wv;
 
   if constexpr (MODE == PASS_B) {
     if (w >= n_wg) {  // S partial + snapshot of p for fin_kernel (which updates p in place)
@@ -226,6 +251,10 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       const long long c0 = tot * sw / nsw, c1 = tot * (sw + 1) / nsw;
       for (long long idx = c0 + tid; idx < c1; idx += NT)
         pold[(size_t)b * tot + idx] = pr[(size_t)b * tot + idx];
+      st_.mark(1);
+      st_.mark(2);
+      st_.mark(3);
+      st_.flush(3, wave_id, lane);
       return;
     }
   }
@@ -241,24 +270,25 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   // Record stream: lane l < 16 holds int l of the chunk's 4 records (i, j, k, w), lane 16 the
   // chunk's partial row, lane 17 its V slot; the other lanes read them by readlane / shuffle, so
   // no register array is indexed at run time.
-  constexpr int DR = 6;  // records this many chunks ahead
+  // Ring of U record registers: the loop below is unrolled U times so each ring slot keeps a
+  // fixed register (a rotation by register moves would wait for every load in flight).
+  constexpr int U = 6;   // records U - 1 chunks ahead; theta values and c two ahead (ring of 3)
   const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
   const int* __restrict__ rows_i = reinterpret_cast<const int*>(rows);
+  // Every load in the chunk loop is issued by every lane on every path (addresses clamped, values
+  // selected afterwards): an exec-masked load behind a branch would make the compiler's vmcnt
+  // accounting assume it may be missing and wait for everything in flight.
   auto ld_rec = [&](int q) -> int {
     const int l = lane & 31;
-    if (l < 16) return rows_i[(size_t)q * 16 + l];
-    if constexpr (MODE != PASS_LL)
-      if (l == 16) return chunk_prow[q];
-    if constexpr (MODE != PASS_B)
-      if (l == 17) return chunk_vslot[q];
-    return 0;
+    const int* src = l < 16 ? rows_i + (size_t)q * 16 + l : l == 16 ? chunk_prow + q : chunk_vslot + q;
+    return *src;
   };
   auto clampq = [&](int q) { return q < c1 ? q : c1 - 1; };
   const bool any = c0 < c1;
-  int rv[DR + 1];
+  int rv[U];
 #pragma unroll
-  for (int i = 0; i < DR; ++i) rv[i] = any ? ld_rec(clampq(c0 + i)) : 0;
-  rv[DR] = 0;
+  for (int i = 0; i < U - 1; ++i) rv[i] = any ? ld_rec(clampq(c0 + i)) : 0;
+  rv[U - 1] = 0;
 
   if constexpr (MODE != PASS_B) {
     // ---- V_g[b][h] = sum_a th_g[a] p_r[a][b][h] for the workgroup's pivot genes (LDS)
@@ -308,6 +338,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     }
     __syncthreads();
   }
+  st_.mark(1);
 
   double* __restrict__ cb = cbuf + (size_t)b * (n_rows0 + 1);
   double* __restrict__ pb = prows + (size_t)b * n_prows * T::K2;
@@ -320,7 +351,8 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       const int pc = 64 * t + lane;
       const int row8 = pc < 8 * T::KP ? pc / T::KP : 0, col = pc % T::KP;
       const int g = __shfl(rv, (row8 & 3) * 4 + ((row8 >> 2) ? vcomp : ucomp), 64);
-      v[t] = (pc < 8 * T::KP && col < K) ? th[(size_t)g * K + col] : 0.0;
+      const double x = th[(size_t)g * K + (col < K ? col : K - 1)];
+      v[t] = (pc < 8 * T::KP && col < K) ? x : 0.0;
     }
   };
   auto stage_store = [&](double* I, const double (&v)[T::NPC]) {
@@ -346,87 +378,84 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     return hi == 0 ? w0 : hi == 1 ? w1 : hi == 2 ? w2 : w3;
   };
   if (any) {
-    // Software pipeline, deep enough to cover an L2 / MALL round trip with a few chunks of work:
-    // records + metadata DR chunks ahead, theta values (and c) three ahead, the LDS image of the
-    // next chunk written at the end of this one (double buffer).
-    double st[3][T::NPC];  // theta values of chunks q + 1, q + 2, q + 3
+    // Software pipeline: records U - 1 chunks ahead, theta values (and c) two ahead; the LDS
+    // image of chunk q + 1 is written at the end of chunk q (double buffer).
+    double st[3][T::NPC];  // theta values of chunk q in slot (q - c0) % 3
+    double cr[3] = {0.0, 0.0, 0.0};  // PASS_B: c of observation hi, same slots
     stage_load(rv[0], st[0]);
-    stage_store(img, st[0]);
-    stage_load(rv[1], st[0]);
-    stage_load(rv[2], st[1]);
-    double cn[4] = {0.0, 0.0, 0.0, 0.0};  // PASS_B: c of observation hi of chunks q .. q + 3
+    stage_load(rv[1], st[1]);
     if constexpr (MODE == PASS_B) {
-      cn[0] = cb[rec_w(rv[0])];
-      cn[1] = cb[rec_w(rv[1])];
-      cn[2] = cb[rec_w(rv[2])];
+      cr[0] = cb[rec_w(rv[0])];
+      cr[1] = cb[rec_w(rv[1])];
     }
-    for (int q = c0; q < c1; ++q) {
-      const int buf = (q - c0) & 1;
-      rv[DR] = ld_rec(clampq(q + DR));
-      stage_load(rv[3], st[2]);
-      if constexpr (MODE == PASS_B) cn[3] = cb[rec_w(rv[3])];
-      wave_lds_sync();
-      const double* I = img + buf * T::IMG;
-      const int pr0 = __builtin_amdgcn_readlane(rv[0], 16);
-      const int pr1 = __builtin_amdgcn_readlane(rv[1], 16);
+    stage_store(img, st[0]);
+    for (int q0 = c0; q0 < c1; q0 += U) {
+#pragma unroll
+      for (int ph = 0; ph < U; ++ph) {
+        const int q = q0 + ph;
+        if (q >= c1) break;
+        const int buf = ph & 1;  // U is even: the image buffer alternates with q
+        // prefetch: records of chunk q + U - 1 into the slot chunk q - 1 used, theta / c of q + 2
+        rv[(ph + U - 1) % U] = ld_rec(clampq(q + U - 1));
+        stage_load(rv[(ph + 2) % U], st[(ph + 2) % 3]);
+        if constexpr (MODE == PASS_B) cr[(ph + 2) % 3] = cb[rec_w(rv[(ph + 2) % U])];
+        wave_lds_sync();
+        const double* I = img + buf * T::IMG;
+        const int rq = rv[ph % U];
+        const int pr0 = __builtin_amdgcn_readlane(rq, 16);
+        const int pr1 = __builtin_amdgcn_readlane(rv[(ph + 1) % U], 16);
 
-      double c = cn[0];
-      if constexpr (MODE != PASS_B) {
-        // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
-        const int nw = rec_w(rv[0]);
-        const double* __restrict__ V = Vt + __builtin_amdgcn_readlane(rv[0], 17) * T::VDBL;
-        double dp = 0.0;
+        double c = cr[ph % 3];
+        if constexpr (MODE != PASS_B) {
+          // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
+          const int nw = rec_w(rq);
+          const double* __restrict__ V = Vt + __builtin_amdgcn_readlane(rq, 17) * T::VDBL;
+          double dp = 0.0;
 #pragma unroll
-        for (int bg = 0; bg < T::NBG; ++bg) {
-          double z = 0.0;
+          for (int bg = 0; bg < T::NBG; ++bg) {
+            double z = 0.0;
 #pragma unroll
-          for (int hs = 0; hs < NG; ++hs)
-            z = mfma4(I[(4 + lo) * TR + 4 * hs + hi], V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
-          dp = fma(I[hi * TR + 16 * bg + 4 * blk + lo], z, dp);
+            for (int hs = 0; hs < NG; ++hs)
+              z = mfma4(I[(4 + lo) * TR + 4 * hs + hi], V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
+            dp = fma(I[hi * TR + 16 * bg + 4 * blk + lo], z, dp);
+          }
+          const double d = row16_sum(dp) + eps;
+          if constexpr (MODE == PASS_LL) {
+            if ((lane & 15) == 0) ll += (double)nw * log(d);
+          } else {
+            c = (double)nw / d;
+            cb[(size_t)q * CH + hi] = c;  // the 16 lanes of row hi store the same value
+          }
         }
-        const double d = row16_sum(dp) + eps;
-        if constexpr (MODE == PASS_LL) {
-          if ((lane & 15) == 0) ll += (double)nw * log(d);
-        } else {
-          c = (double)nw / d;
-          if ((lane & 15) == 0) cb[(size_t)q * CH + hi] = c;
-        }
-      }
-      if constexpr (MODE != PASS_LL) {
-        // ---- M += c th_u (x) th_v over the chunk's 4 observations
-#pragma unroll
-        for (int ts = 0; ts < T::NTS; ++ts) {
-          const int t = 4 * ts + blk;
-          const bool tv = t < NG * NG;
-          const int xs = tv ? t / NG : 0, ys = tv ? t % NG : 0;
-          const double av = tv ? c * I[hi * TR + 4 * xs + lo] : 0.0;
-          macc[ts] = mfma4(av, I[(4 + hi) * TR + 4 * ys + lo], macc[ts]);
-        }
-        if (q + 1 >= c1 || pr1 != pr0) {  // end of this gene stretch: its partial row
-          double* __restrict__ out = pb + (size_t)pr0 * T::K2;
+        if constexpr (MODE != PASS_LL) {
+          // ---- M += c th_u (x) th_v over the chunk's 4 observations
 #pragma unroll
           for (int ts = 0; ts < T::NTS; ++ts) {
             const int t = 4 * ts + blk;
-            const int x = 4 * (t / NG) + hi, y = 4 * (t % NG) + lo;
-            if (t < NG * NG && x < K && y < K) out[x * K + y] = macc[ts];
-            macc[ts] = 0.0;
+            const bool tv = t < NG * NG;
+            const int xs = tv ? t / NG : 0, ys = tv ? t % NG : 0;
+            const double av = tv ? c * I[hi * TR + 4 * xs + lo] : 0.0;
+            macc[ts] = mfma4(av, I[(4 + hi) * TR + 4 * ys + lo], macc[ts]);
+          }
+          if (q + 1 >= c1 || pr1 != pr0) {  // end of this gene stretch: its partial row
+            double* __restrict__ out = pb + (size_t)pr0 * T::K2;
+#pragma unroll
+            for (int ts = 0; ts < T::NTS; ++ts) {
+              const int t = 4 * ts + blk;
+              const int x = 4 * (t / NG) + hi, y = 4 * (t % NG) + lo;
+              if (t < NG * NG && x < K && y < K) out[x * K + y] = macc[ts];
+              macc[ts] = 0.0;
+            }
           }
         }
+        // next chunk's image into the other buffer (its reads of this buffer are done)
+        wave_lds_sync();
+        stage_store(img + (buf ^ 1) * T::IMG, st[(ph + 1) % 3]);
       }
-      // next chunk's image into the other buffer (its reads of this buffer are done)
-      wave_lds_sync();
-      stage_store(img + (buf ^ 1) * T::IMG, st[0]);
-#pragma unroll
-      for (int t = 0; t < T::NPC; ++t) {
-        st[0][t] = st[1][t];
-        st[1][t] = st[2][t];
-      }
-#pragma unroll
-      for (int i = 0; i < DR; ++i) rv[i] = rv[i + 1];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) cn[i] = cn[i + 1];
     }
   }
+  st_.mark(2);
+  st_.t[5] = (unsigned long long)(c1 - c0);
   if constexpr (MODE == PASS_LL) {
     // fixed-order workgroup sum of the log-likelihood terms
     __shared__ double red[NW];
@@ -440,6 +469,8 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       partL[(size_t)b * n_wg + w] = t;
     }
   }
+  st_.mark(3);
+  st_.flush(MODE == PASS_B ? 1 : MODE == PASS_A ? 0 : 4, wave_id, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -481,6 +512,8 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
   constexpr int K2 = F::K2, K3 = K * K * K, NG = F::NG;
   extern __shared__ __attribute__((aligned(16))) double Ms[];  // [CB][4 genes][K2P]
   const int tid = threadIdx.x, b = blockIdx.y;
+  Stamp st_{};
+  st_.mark(0);
   if ((int)blockIdx.x < n_gene_wg) {
     const int lane = tid & 63, wv = tid >> 6;
     const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
@@ -493,21 +526,44 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
     double acc[F::NXG];
 #pragma unroll
     for (int xg = 0; xg < F::NXG; ++xg) acc[xg] = 0.0;
+    // partial-row ranges of the 4 genes for every combo (= s * R + r), once, in LDS
+    __shared__ int pp[3 * MAX_R][5];
+    if (tid < NC * 5) {
+      const int c = tid / 5, i = tid % 5;
+      pp[c][i] = prow_ptr[(size_t)c * (P + 1) + (g0 + i < P ? g0 + i : P)];
+    }
     for (int cb0 = 0; cb0 < NC; cb0 += F::CB) {
       const int ncb = NC - cb0 < F::CB ? NC - cb0 : F::CB;
+      const int NE = ncb * 4 * F::K2P;
       __syncthreads();
-      for (int idx = tid; idx < ncb * 4 * F::K2P; idx += FIN_NT) {
-        const int c = idx / (4 * F::K2P), rem = idx % (4 * F::K2P);
-        const int gl = rem / F::K2P, k = rem % F::K2P;
-        const int g = g0 + gl;
-        double m = 0.0;
-        if (g < P && k < K2) {
-          const int* ptr = prow_ptr + (size_t)(cb0 + c) * (P + 1);  // combo = s * R + r
-          for (int q = ptr[g]; q < ptr[g + 1]; ++q) m += pb[(size_t)q * K2 + k];
+      // Ms[c][gene][k] = the gene's partial rows summed in row order; four entries per thread
+      // per round, their first two rows loaded together (addresses clamped, loads unconditional)
+      for (int i0 = tid; i0 < NE; i0 += 4 * FIN_NT) {
+        int qa[4], qb[4], kk[4];
+        double v1[4], v2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = i0 + u * FIN_NT;
+          const int c = idx / (4 * F::K2P), rem = idx % (4 * F::K2P);
+          const int gl = rem / F::K2P, k = rem % F::K2P;
+          const bool ok = idx < NE && k < K2;
+          qa[u] = ok ? pp[cb0 + c][gl] : 0;
+          qb[u] = ok ? pp[cb0 + c][gl + 1] : 0;
+          kk[u] = k < K2 ? k : 0;
+          v1[u] = pb[(size_t)(qa[u] < qb[u] ? qa[u] : 0) * K2 + kk[u]];
+          v2[u] = pb[(size_t)(qa[u] + 1 < qb[u] ? qa[u] + 1 : 0) * K2 + kk[u]];
         }
-        Ms[idx] = m;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = i0 + u * FIN_NT;
+          double m = qa[u] < qb[u] ? v1[u] : 0.0;
+          if (qa[u] + 1 < qb[u]) m += v2[u];
+          for (int q = qa[u] + 2; q < qb[u]; ++q) m += pb[(size_t)q * K2 + kk[u]];
+          if (idx < NE) Ms[idx] = m;
+        }
       }
       __syncthreads();
+      st_.mark(1);
       for (int item = wv; item < ncb * F::NXG; item += 4) {
         const int c = item / F::NXG, xg = item % F::NXG;
         const int combo = cb0 + c, s = combo / R, r = combo % R;
@@ -543,6 +599,7 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
       }
     }
     // X[gene hi][x = 4 (4 xg + blk) + lo]: the four waves' partials summed in wave order
+    st_.mark(2);
     __syncthreads();
 #pragma unroll
     for (int xg = 0; xg < F::NXG; ++xg) Ms[(wv * F::NXG + xg) * 64 + lane] = acc[xg];
@@ -561,6 +618,8 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
         }
       }
     }
+    st_.mark(3);
+    st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 4 + wv, lane);
   } else {
     // 64 cells per workgroup, four threads per cell, each summing a quarter of the rating's S
     // partials (eight loads in flight), the quarters combined in order through LDS
@@ -724,6 +783,7 @@ struct Launch {
 }  // namespace
 
 struct mmsbm_ctx {
+  unsigned long long* stamp = nullptr;  // MMSBM_STAMP measurement builds
   int device = 0;
   int K = 0, R = 0, B = 0, P = 0;
   double eps = 1e-10;
@@ -956,6 +1016,13 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
     return fail(MMSBM_ERR_INVALID, "device %d outside [0, %d)", device, ndev);
   auto* c = new mmsbm_ctx();
   c->device = device;
+  if (MMSBM_STAMP && getenv("MMSBM_STAMP")) {
+    DeviceGuard g(device);
+    const size_t bytes = sizeof(unsigned long long) * 5 * STAMP_WAVES * STAMP_SLOTS;
+    HIP_TRY(hipMalloc(&c->stamp, bytes));
+    HIP_TRY(hipMemset(c->stamp, 0, bytes));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), &c->stamp, sizeof(c->stamp)));
+  }
   *out = c;
   return MMSBM_OK;
 }
@@ -965,6 +1032,7 @@ int mmsbm_destroy(mmsbm_ctx* c) {
   DeviceGuard g(c->device);
   for (auto& s : c->sets) s.release();
   if (c->deg) (void)hipFree(c->deg);
+  if (c->stamp) (void)hipFree(c->stamp);
   for (auto& v : c->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   delete c;
@@ -1106,6 +1174,36 @@ int mmsbm_iterate(mmsbm_ctx* c, double* theta, double* pr, int32_t n_iters, void
   hipStream_t s = (hipStream_t)stream;
   for (int it = 0; it < n_iters; ++it)
     if ((rc = one_iteration(c, theta, pr, c->timing && it % c->timing_stride == 0, s))) return rc;
+  if (c->stamp && n_iters > 0) {  // measurement: phase cycles of the last iteration's waves
+    std::vector<unsigned long long> h((size_t)5 * STAMP_WAVES * STAMP_SLOTS);
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemcpy(h.data(), c->stamp, h.size() * 8, hipMemcpyDeviceToHost));
+    const char* names[5] = {"passA", "passB", "fin", "spart", "passLL"};
+    for (int k = 0; k < 5; ++k) {
+      double sum[4] = {0, 0, 0, 0}, chunks = 0;
+      unsigned long long mx = 0, t0min = ~0ull, t3max = 0;
+      long long n = 0;
+      for (long long wv = 0; wv < STAMP_WAVES; ++wv) {
+        const unsigned long long* t = &h[((size_t)k * STAMP_WAVES + wv) * STAMP_SLOTS];
+        if (t[0] == 0) continue;
+        ++n;
+        sum[0] += (double)(t[1] - t[0]);
+        sum[1] += (double)(t[2] - t[1]);
+        sum[2] += (double)(t[3] - t[2]);
+        sum[3] += (double)(t[3] - t[0]);
+        chunks += (double)t[5];
+        mx = std::max(mx, t[3] - t[0]);
+        t0min = std::min(t0min, t[0]);
+        t3max = std::max(t3max, t[3]);
+      }
+      if (n)
+        fprintf(stderr, "[mmsbm stamp] %-6s waves %6lld  avg cycles: phase1 %8.0f  phase2 %8.0f  "
+                "phase3 %8.0f  life %8.0f  (max %llu, first start -> last end %llu, chunks/wave %.1f)\n",
+                names[k], n, sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n, mx, t3max - t0min,
+                chunks / n);
+    }
+    HIP_TRY(hipMemset(c->stamp, 0, h.size() * 8));
+  }
   return MMSBM_OK;
 }
 
