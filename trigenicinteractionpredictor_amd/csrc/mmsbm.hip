@@ -39,6 +39,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -82,13 +83,15 @@ struct KT {
   static constexpr int KP = 4 * NG;
   static constexpr int K2 = K * K, K3 = K * K * K;
   static constexpr int NBG = (NG + 3) / 4;        // Z phase: groups of 4 b-tiles (one per block)
-  static constexpr int NTS = (NG * NG + 3) / 4;   // M phase: MFMA steps of 4 (x, y) tiles
+  static constexpr int NGB = (NG + 3) / 4;        // M phase: groups of 4 y tiles (one per block)
+  static constexpr int NTS = NG * NGB;            // M phase steps: x tile ts / NGB, y tiles 4 (ts % NGB) + blk
   static constexpr int VROWS = 16 * NBG;          // V image rows (b); zero from K on
   static constexpr int VR = KP + 2;               // row stride: 2 x odd doubles, conflict-free B reads
   static constexpr int VDBL = VROWS * VR;         // one gene's V image
   static constexpr int TR = KP + 2;               // theta image row stride
   static constexpr int IMG = 8 * TR;              // one chunk: th_u rows of obs 0-3, th_v rows
-  static constexpr int NPC = (8 * KP + 63) / 64;  // staged doubles per lane per chunk
+  static constexpr int SW = (K % 2 == 0) ? 2 : 1;  // staging width: double2 pieces when K is even
+  static constexpr int NPC = (8 * KP / SW + 63) / 64;  // staged pieces per lane per chunk
   static constexpr int IMG_BYTES = NW * 2 * IMG * 8;
   static constexpr int GMAX_RAW = (lds_target(K) - IMG_BYTES - 64) / ((VDBL + KP) * 8);
   static constexpr int GMAX = GMAX_RAW > 64 ? 64 : (GMAX_RAW < 4 ? 4 : GMAX_RAW);
@@ -101,6 +104,7 @@ struct KT {
   static constexpr int NSI = NSI_ALL < 8 ? NSI_ALL : 8;           // accumulators per wave
   static constexpr int NIG = (NG * NCG + NW * NSI - 1) / (NW * NSI);  // item groups (workgroups)
   static_assert(LDS_A <= 160 * 1024, "pass A LDS over budget");
+  static_assert(64 * KP * 8 <= IMG_BYTES, "S partial staging over the pass B LDS");
 };
 
 int gmax_for(int K);  // host view of KT<K>::GMAX (table below)
@@ -175,27 +179,55 @@ enum { PASS_A = 0, PASS_LL = 1, PASS_B = 2 };
 template <int K>
 __device__ __forceinline__ void s_partial(const double* __restrict__ th, const double* __restrict__ prows_b,
                                           const int* __restrict__ prow_gene, int q0, int q1,
-                                          double* __restrict__ out, int ig, int wv, int hi, int blk,
-                                          int lo) {
+                                          double* __restrict__ out, double* __restrict__ Tq, int ig,
+                                          int tid, int wv, int hi, int blk, int lo) {
   using T = KT<K>;
+  // blocks of QB partial rows: their genes' theta rows staged in LDS (zero padded), so the loop
+  // over the block only streams the partial rows themselves from HBM
+  constexpr int QB = 64, NI = (QB * T::KP + NT - 1) / NT;
   double acc[T::NSI];
 #pragma unroll
   for (int k = 0; k < T::NSI; ++k) acc[k] = 0.0;
-#pragma unroll 4
-  for (int q = q0; q < q1; q += 4) {
-    const int qi = q + hi;
-    const bool vq = qi < q1;
-    const int g = vq ? prow_gene[qi] : 0;
-    const double* __restrict__ Mq = prows_b + (size_t)(vq ? qi : q0) * T::K2;
+  for (int qb = q0; qb < q1; qb += QB) {
+    const int nq = q1 - qb < QB ? q1 - qb : QB;
+    __syncthreads();
+    double x[NI];
 #pragma unroll
-    for (int k = 0; k < T::NSI; ++k) {
-      const int it = ig * NW * T::NSI + wv + NW * k;
-      if (it < T::NG * T::NCG) {
-        const int at = it / T::NCG, cg = it % T::NCG;
-        const int a = 4 * at + lo, cell = 4 * (4 * cg + blk) + lo;
-        const double av = (vq && a < K) ? th[(size_t)g * K + a] : 0.0;
-        const double bv = (vq && cell < T::K2) ? Mq[cell] : 0.0;
-        acc[k] = mfma4(av, bv, acc[k]);
+    for (int i = 0; i < NI; ++i) {
+      const int idx = tid + NT * i, ql = idx / T::KP, a = idx % T::KP;
+      const int g = prow_gene[qb + (ql < nq ? ql : 0)];
+      const double v = th[(size_t)g * K + (a < K ? a : 0)];
+      x[i] = (idx < QB * T::KP && ql < nq && a < K) ? v : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      if (tid + NT * i < QB * T::KP) Tq[tid + NT * i] = x[i];
+    __syncthreads();
+    for (int qq = 0; qq < nq; qq += 16) {  // 4 MFMA steps per round, their loads issued together
+      double m[4][T::NSI];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool vq = qq + 4 * u + hi < nq;
+        const double* __restrict__ Mq = prows_b + (size_t)(qb + (vq ? qq + 4 * u + hi : 0)) * T::K2;
+#pragma unroll
+        for (int k = 0; k < T::NSI; ++k) {
+          const int it = ig * NW * T::NSI + wv + NW * k;
+          const int cg = it % T::NCG, cell = 4 * (4 * cg + blk) + lo;
+          const double v = Mq[cell < T::K2 ? cell : 0];
+          m[u][k] = (vq && cell < T::K2) ? v : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int k = 0; k < T::NSI; ++k) {
+          const int it = ig * NW * T::NSI + wv + NW * k;
+          if (it < T::NG * T::NCG) {
+            const int a = 4 * (it / T::NCG) + lo;
+            // zero for a >= K and for rows past nq (Tq holds QB rows)
+            acc[k] = mfma4(Tq[(qq + 4 * u + hi) * T::KP + a], m[u][k], acc[k]);
+          }
+        }
       }
     }
   }
@@ -246,7 +278,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       const int sw = w - n_wg, sp = sw / T::NIG, ig = sw % T::NIG;
       const int* d = sp_desc + 3 * sp;
       s_partial<K>(th, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
-                   spart + ((size_t)b * n_sp + sp) * T::K3, ig, wv, hi, blk, lo);
+                   spart + ((size_t)b * n_sp + sp) * T::K3, smem, ig, tid, wv, hi, blk, lo);
       const long long tot = (long long)R * T::K3, nsw = (long long)n_sp * T::NIG;
       const long long c0 = tot * sw / nsw, c1 = tot * (sw + 1) / nsw;
       for (long long idx = c0 + tid; idx < c1; idx += NT)
@@ -345,21 +377,27 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   // record components: lane l holds int (l & 15) of the chunk's 4 records (i, j, k, w) and the
   // others read it with a lane shuffle: no register array is indexed at run time
   const int ucomp = s == 0 ? 1 : 0, vcomp = s == 2 ? 1 : 2;
-  auto stage_load = [&](int rv, double (&v)[T::NPC]) {
+  // staged pieces of one chunk: piece pc = 64 t + lane is SW doubles of row8 = pc / (KP / SW)
+  // (rows 0-3: th_u of obs 0-3, rows 4-7: th_v), columns SW (pc % (KP / SW)) ..
+  using SV = typename std::conditional<T::SW == 2, double2, double>::type;
+  constexpr int PR = T::KP / T::SW;  // pieces per image row
+  auto stage_load = [&](int rv, SV (&v)[T::NPC]) {
 #pragma unroll
     for (int t = 0; t < T::NPC; ++t) {
       const int pc = 64 * t + lane;
-      const int row8 = pc < 8 * T::KP ? pc / T::KP : 0, col = pc % T::KP;
+      const int row8 = pc < 8 * PR ? pc / PR : 0, col = T::SW * (pc % PR);
       const int g = __shfl(rv, (row8 & 3) * 4 + ((row8 >> 2) ? vcomp : ucomp), 64);
-      const double x = th[(size_t)g * K + (col < K ? col : K - 1)];
-      v[t] = (pc < 8 * T::KP && col < K) ? x : 0.0;
+      const bool ok = pc < 8 * PR && col < K;
+      const SV x = *reinterpret_cast<const SV*>(th + (size_t)g * K + (col < K ? col : K - T::SW));
+      if constexpr (T::SW == 2) v[t] = ok ? x : make_double2(0.0, 0.0);
+      else v[t] = ok ? x : 0.0;
     }
   };
-  auto stage_store = [&](double* I, const double (&v)[T::NPC]) {
+  auto stage_store = [&](double* I, const SV (&v)[T::NPC]) {
 #pragma unroll
     for (int t = 0; t < T::NPC; ++t) {
       const int pc = 64 * t + lane;
-      if (pc < 8 * T::KP) I[(pc / T::KP) * TR + pc % T::KP] = v[t];
+      if (pc < 8 * PR) *reinterpret_cast<SV*>(I + (pc / PR) * TR + T::SW * (pc % PR)) = v[t];
     }
   };
 
@@ -372,15 +410,11 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   wave_lds_sync();
 
   // w of observation hi (count on stream 0, c index on streams 1 / 2) of a record register
-  auto rec_w = [&](int r) {
-    const int w0 = __builtin_amdgcn_readlane(r, 3), w1 = __builtin_amdgcn_readlane(r, 7);
-    const int w2 = __builtin_amdgcn_readlane(r, 11), w3 = __builtin_amdgcn_readlane(r, 15);
-    return hi == 0 ? w0 : hi == 1 ? w1 : hi == 2 ? w2 : w3;
-  };
+  auto rec_w = [&](int r) { return __shfl(r, hi * 4 + 3, 64); };
   if (any) {
     // Software pipeline: records U - 1 chunks ahead, theta values (and c) two ahead; the LDS
     // image of chunk q + 1 is written at the end of chunk q (double buffer).
-    double st[3][T::NPC];  // theta values of chunk q in slot (q - c0) % 3
+    SV st[3][T::NPC];  // theta values of chunk q in slot (q - c0) % 3
     double cr[3] = {0.0, 0.0, 0.0};  // PASS_B: c of observation hi, same slots
     stage_load(rv[0], st[0]);
     stage_load(rv[1], st[1]);
@@ -410,13 +444,16 @@ __global__ __launch_bounds__(NT) void pass_kernel(
           // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
           const int nw = rec_w(rq);
           const double* __restrict__ V = Vt + __builtin_amdgcn_readlane(rq, 17) * T::VDBL;
+          double az[NG];  // th_v[obs lo][4 hs + hi]: the A operand of every b group
+#pragma unroll
+          for (int hs = 0; hs < NG; ++hs) az[hs] = I[(4 + lo) * TR + 4 * hs + hi];
           double dp = 0.0;
 #pragma unroll
           for (int bg = 0; bg < T::NBG; ++bg) {
             double z = 0.0;
 #pragma unroll
             for (int hs = 0; hs < NG; ++hs)
-              z = mfma4(I[(4 + lo) * TR + 4 * hs + hi], V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
+              z = mfma4(az[hs], V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
             dp = fma(I[hi * TR + 16 * bg + 4 * blk + lo], z, dp);
           }
           const double d = row16_sum(dp) + eps;
@@ -429,21 +466,25 @@ __global__ __launch_bounds__(NT) void pass_kernel(
         }
         if constexpr (MODE != PASS_LL) {
           // ---- M += c th_u (x) th_v over the chunk's 4 observations
+          // step ts: x tile ts / NGB (the same in every block), y tile 4 (ts % NGB) + blk, so a
+          // lane reads NG A values and NGB B values per chunk
+          double au[NG], bvv[T::NGB];
 #pragma unroll
-          for (int ts = 0; ts < T::NTS; ++ts) {
-            const int t = 4 * ts + blk;
-            const bool tv = t < NG * NG;
-            const int xs = tv ? t / NG : 0, ys = tv ? t % NG : 0;
-            const double av = tv ? c * I[hi * TR + 4 * xs + lo] : 0.0;
-            macc[ts] = mfma4(av, I[(4 + hi) * TR + 4 * ys + lo], macc[ts]);
+          for (int xs = 0; xs < NG; ++xs) au[xs] = c * I[hi * TR + 4 * xs + lo];
+#pragma unroll
+          for (int j = 0; j < T::NGB; ++j) {
+            const int ys = 4 * j + blk;
+            const double v = I[(4 + hi) * TR + (ys < NG ? 4 * ys + lo : 0)];
+            bvv[j] = ys < NG ? v : 0.0;
           }
+#pragma unroll
+          for (int ts = 0; ts < T::NTS; ++ts) macc[ts] = mfma4(au[ts / T::NGB], bvv[ts % T::NGB], macc[ts]);
           if (q + 1 >= c1 || pr1 != pr0) {  // end of this gene stretch: its partial row
             double* __restrict__ out = pb + (size_t)pr0 * T::K2;
 #pragma unroll
             for (int ts = 0; ts < T::NTS; ++ts) {
-              const int t = 4 * ts + blk;
-              const int x = 4 * (t / NG) + hi, y = 4 * (t % NG) + lo;
-              if (t < NG * NG && x < K && y < K) out[x * K + y] = macc[ts];
+              const int x = 4 * (ts / T::NGB) + hi, y = 4 * (4 * (ts % T::NGB) + blk) + lo;
+              if (x < K && y < K) out[x * K + y] = macc[ts];
               macc[ts] = 0.0;
             }
           }
@@ -496,10 +537,44 @@ struct FT {
   static constexpr int NXG = (NG + 3) / 4;      // MFMA groups of 4 x tiles
   static constexpr int CB_RAW = (60 * 1024) / (4 * K2P * 8);
   static constexpr int CB = CB_RAW > 6 ? 6 : (CB_RAW < 1 ? 1 : CB_RAW);  // combos staged at once
-  static constexpr int MS = CB * 4 * K2P > 4 * NXG * 64 ? CB * 4 * K2P : 4 * NXG * 64;  // doubles
+  static constexpr int MS_G = CB * 4 * K2P > 4 * NXG * 64 ? CB * 4 * K2P : 4 * NXG * 64;
+  static constexpr int MS = MS_G > MAX_R * 4 * 64 ? MS_G : MAX_R * 4 * 64;  // doubles
   static constexpr bool PLDS = K <= 12;  // p of every rating staged in LDS (else read from L2)
   static constexpr int LDS = (MS + (PLDS ? MAX_R * K * K * K : 0)) * 8;
 };
+
+// One (combo, x group) item of the fin gene part: sum_k M_g[k] P^s[k][x] over the dense (y, z)
+// cells k on MFMA (k = 4 ks + hi).  P^s[k][x]: s = 0 p[x][y][z] = p[x K2 + k], s = 1 p[y][x][z]
+// (k = y K + z), s = 2 p[y][z][x] = p[k K + x].  Addresses are clamped (k >= K2: M is zero there;
+// x >= K: the column is never stored), so every load is unconditional and a round's loads go out
+// together.
+template <int K, int S>
+__device__ __forceinline__ double x_item(const double* __restrict__ Mg, const double* __restrict__ p,
+                                         int x, int hi) {
+  using F = FT<K>;
+  constexpr int K2 = K * K, UB = F::PLDS ? 8 : 16;
+  const int xc = x < K ? x : K - 1;
+  double a2 = 0.0;
+#pragma unroll 1
+  for (int ks0 = 0; ks0 < F::KS; ks0 += UB) {
+    double av[UB], bv[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int ks = ks0 + u < F::KS ? ks0 + u : F::KS - 1;
+      const int k = 4 * ks + hi, kc = k < K2 ? k : K2 - 1;
+      int idx;
+      if constexpr (S == 0) idx = xc * K2 + kc;
+      else if constexpr (S == 2) idx = kc * K + xc;
+      else idx = kc + (kc / K) * (K2 - K) + xc * K;
+      const double m = Mg[k];
+      av[u] = ks0 + u < F::KS ? m : 0.0;
+      bv[u] = p[idx];
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) a2 = mfma4(av[u], bv[u], a2);
+  }
+  return a2;
+}
 
 template <int K, bool SUMS>
 __global__ __launch_bounds__(FIN_NT) void fin_kernel(
@@ -521,28 +596,50 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
     const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
     const int NC = 3 * R;
     double* Ps = Ms + F::MS;  // [R][K3] when F::PLDS
-    if constexpr (F::PLDS)
-      for (int idx = tid; idx < R * K3; idx += FIN_NT) Ps[idx] = pold[(size_t)b * R * K3 + idx];
+    // epilogue operands (wave 0: gene g0 + hi, x = 4 (4 xg + blk) + lo), loaded up front
+    const int ge = g0 + hi < P ? g0 + hi : P - 1;
+    double th_e[F::NXG];
+#pragma unroll
+    for (int xg = 0; xg < F::NXG; ++xg) {
+      const int x = 4 * (4 * xg + blk) + lo;
+      th_e[xg] = theta[((size_t)b * P + ge) * K + (x < K ? x : 0)];
+    }
+    const int deg_e = deg[ge];
+    // partial-row ranges of the 4 genes for every combo (= s * R + r) and p, staged in LDS with
+    // all their loads in flight together
+    __shared__ int pp[3 * MAX_R][5];
+    {
+      const int c = tid / 5, i = tid % 5;
+      const int v = prow_ptr[(size_t)(c < NC ? c : 0) * (P + 1) + (g0 + i < P ? g0 + i : P)];
+      if constexpr (F::PLDS) {
+        for (int base = 0; base < R * K3; base += 8 * FIN_NT) {
+          double pv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int idx = base + u * FIN_NT + tid;
+            pv[u] = pold[(size_t)b * R * K3 + (idx < R * K3 ? idx : 0)];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (base + u * FIN_NT + tid < R * K3) Ps[base + u * FIN_NT + tid] = pv[u];
+        }
+      }
+      if (tid < NC * 5) pp[c][i] = v;
+    }
     double acc[F::NXG];
 #pragma unroll
     for (int xg = 0; xg < F::NXG; ++xg) acc[xg] = 0.0;
-    // partial-row ranges of the 4 genes for every combo (= s * R + r), once, in LDS
-    __shared__ int pp[3 * MAX_R][5];
-    if (tid < NC * 5) {
-      const int c = tid / 5, i = tid % 5;
-      pp[c][i] = prow_ptr[(size_t)c * (P + 1) + (g0 + i < P ? g0 + i : P)];
-    }
     for (int cb0 = 0; cb0 < NC; cb0 += F::CB) {
       const int ncb = NC - cb0 < F::CB ? NC - cb0 : F::CB;
       const int NE = ncb * 4 * F::K2P;
       __syncthreads();
-      // Ms[c][gene][k] = the gene's partial rows summed in row order; four entries per thread
+      // Ms[c][gene][k] = the gene's partial rows summed in row order; eight entries per thread
       // per round, their first two rows loaded together (addresses clamped, loads unconditional)
-      for (int i0 = tid; i0 < NE; i0 += 4 * FIN_NT) {
-        int qa[4], qb[4], kk[4];
-        double v1[4], v2[4];
+      for (int i0 = tid; i0 < NE; i0 += 8 * FIN_NT) {
+        int qa[8], qb[8], kk[8];
+        double v1[8], v2[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const int idx = i0 + u * FIN_NT;
           const int c = idx / (4 * F::K2P), rem = idx % (4 * F::K2P);
           const int gl = rem / F::K2P, k = rem % F::K2P;
@@ -554,7 +651,7 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
           v2[u] = pb[(size_t)(qa[u] + 1 < qb[u] ? qa[u] + 1 : 0) * K2 + kk[u]];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const int idx = i0 + u * FIN_NT;
           double m = qa[u] < qb[u] ? v1[u] : 0.0;
           if (qa[u] + 1 < qb[u]) m += v2[u];
@@ -570,29 +667,8 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
         const double* __restrict__ p = (F::PLDS ? Ps : pold + (size_t)b * R * K3) + (size_t)r * K3;
         const int x = 4 * (4 * xg + blk) + lo;
         const double* __restrict__ Mg = Ms + ((size_t)c * 4 + lo) * F::K2P;
-        // B operand P^s[k][x]: s = 0 p[x][y][z] = p[x K2 + k], s = 2 p[y][z][x] = p[k K + x],
-        // s = 1 p[y][x][z] (k = y K + z).  Four k-steps per round: their loads go out together.
-        auto pidx = [&](int k) {
-          if (s == 0) return x * K2 + k;
-          if (s == 2) return k * K + x;
-          const int y = k / K;
-          return (y * K + x) * K + (k - y * K);
-        };
-        const bool xv = x < K;
-        double a2 = 0.0;
-#pragma unroll 1
-        for (int ks = 0; ks < F::KS; ks += 4) {
-          double av[4], bv[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int k = 4 * (ks + u) + hi;
-            const bool ok = ks + u < F::KS;
-            av[u] = ok ? Mg[k] : 0.0;
-            bv[u] = (ok && xv && k < K2) ? p[pidx(k)] : 0.0;
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) a2 = mfma4(av[u], bv[u], a2);
-        }
+        const double a2 = s == 0 ? x_item<K, 0>(Mg, p, x, hi)
+                                 : s == 1 ? x_item<K, 1>(Mg, p, x, hi) : x_item<K, 2>(Mg, p, x, hi);
 #pragma unroll
         for (int q = 0; q < F::NXG; ++q)
           if (q == xg) acc[q] += a2;
@@ -614,48 +690,61 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
         if (g < P && x < K) {
           const size_t o = ((size_t)b * P + g) * K + x;
           if constexpr (SUMS) nth_out[o] = X;
-          else theta[o] = theta[o] * X / (double)deg[g];
+          else theta[o] = th_e[xg] * X / (double)deg_e;
         }
       }
     }
     st_.mark(3);
     st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 4 + wv, lane);
   } else {
-    // 64 cells per workgroup, four threads per cell, each summing a quarter of the rating's S
-    // partials (eight loads in flight), the quarters combined in order through LDS
+    // 64 cells per workgroup, four threads per cell, each summing a quarter of every rating's S
+    // partials (16 loads in flight), the quarters combined in order through LDS
     const int cl = tid & 63, part = tid >> 6;
     const int cell = (blockIdx.x - n_gene_wg) * 64 + cl;
     const bool cv = cell < K3;
-    double npr[MAX_R];
-    double den = eps;
+    const int cc = cv ? cell : 0;
+    double po[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) po[r] = pold[((size_t)b * R + (r < R ? r : R - 1)) * K3 + cc];
     for (int r = 0; r < R; ++r) {
       const int n = spr.hi[r] - spr.lo[r];
       const int s0 = spr.lo[r] + n * part / 4, s1 = spr.lo[r] + n * (part + 1) / 4;
       double S = 0.0;
-      for (int sp = s0; sp < s1; sp += 8) {
-        double v[8];
+      for (int sp = s0; sp < s1; sp += 16) {
+        double v[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          v[u] = (cv && sp + u < s1) ? spart[((size_t)b * n_sp + sp + u) * K3 + cell] : 0.0;
+        for (int u = 0; u < 16; ++u) {
+          const double x = spart[((size_t)b * n_sp + (sp + u < s1 ? sp + u : s0)) * K3 + cc];
+          v[u] = sp + u < s1 ? x : 0.0;
+        }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) S += v[u];
+        for (int u = 0; u < 16; ++u) S += v[u];
       }
-      __syncthreads();
-      Ms[part * 64 + cl] = S;
-      __syncthreads();
-      if (part == 0 && cv) {
-        S = ((Ms[cl] + Ms[64 + cl]) + Ms[128 + cl]) + Ms[192 + cl];
-        if constexpr (SUMS) {
-          S_out[((size_t)b * R + r) * K3 + cell] = S;
-        } else {
-          npr[r] = pold[((size_t)b * R + r) * K3 + cell] * S;
-          den += npr[r];
+      Ms[(r * 4 + part) * 64 + cl] = S;
+    }
+    __syncthreads();
+    if (part == 0 && cv) {
+      double npr[MAX_R];
+      double den = eps;
+#pragma unroll
+      for (int r = 0; r < MAX_R; ++r) {
+        if (r < R) {
+          const double S = ((Ms[r * 256 + cl] + Ms[r * 256 + 64 + cl]) + Ms[r * 256 + 128 + cl]) +
+                           Ms[r * 256 + 192 + cl];
+          if constexpr (SUMS) {
+            S_out[((size_t)b * R + r) * K3 + cell] = S;
+          } else {
+            npr[r] = po[r] * S;
+            den += npr[r];
+          }
         }
       }
+      if constexpr (!SUMS) {
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+          if (r < R) pr[((size_t)b * R + r) * K3 + cell] = npr[r] / den;
+      }
     }
-    if constexpr (!SUMS)
-      if (part == 0 && cv)
-        for (int r = 0; r < R; ++r) pr[((size_t)b * R + r) * K3 + cell] = npr[r] / den;
   }
 }
 
