@@ -1,0 +1,57 @@
+"""Per-wave analysis of a raw s_memtime stamp dump (measurement build, MMSBM_STAMP_DUMP=path).
+
+Layout: u64[5 kernels][65536 waves][8 slots]; slots 0-3 = phase boundaries, 6 = pass prologue loads staged, 4 = genes of the
+wave's workgroup (stream-0 passes), 5 = chunks of the wave's unit.
+"""
+import sys
+
+import numpy as np
+
+NAMES = ["passA", "passB", "fin", "spart", "passLL"]
+
+
+def main(path):
+    h = np.fromfile(path, dtype=np.uint64).reshape(5, 1 << 16, 8).astype(np.int64)
+    for k, name in enumerate(NAMES):
+        t = h[k]
+        ok = t[:, 0] != 0
+        if not ok.any():
+            continue
+        idx = np.nonzero(ok)[0]
+        t = t[ok]
+        t0 = t[:, 0].min()
+        start, end = t[:, 0] - t0, t[:, 3] - t0
+        life = t[:, 3] - t[:, 0]
+        ph1, ph2 = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1]
+        q = lambda a: " ".join("%6d" % v for v in np.percentile(a, [0, 50, 90, 99, 100]))
+        print("%s: %d waves   (percentiles 0/50/90/99/100)" % (name, len(t)))
+        print("  start  %s" % q(start))
+        print("  end    %s" % q(end))
+        print("  life   %s" % q(life))
+        print("  phase1 %s" % q(ph1))
+        print("  phase2 %s" % q(ph2))
+        if name == "fin":
+            print("  ->sync %s" % q(t[:, 4] - t[:, 0]))
+            print("  ->rows %s" % q(t[:, 5] - t[:, 0]))
+        if name in ("passA", "passB", "passLL"):
+            ch = t[:, 5]
+            print("  chunks %s" % q(ch))
+            if ch.max() > 0:
+                a = np.polyfit(ch, ph2, 1)
+                print("  phase2 ~ %.0f cycles/chunk + %.0f" % (a[0], a[1]))
+            if name != "passB":
+                ng = t[:, 4]
+                print("  ->V    %s" % q(t[:, 6] - t[:, 0]))
+                a = np.polyfit(ng, t[:, 6] - t[:, 0], 1)
+                print("  ->V ~ %.0f cycles/gene + %.0f" % (a[0], a[1]))
+                print("  genes  %s" % q(ng))
+                a = np.polyfit(ng, ph1, 1)
+                print("  phase1 ~ %.0f cycles/gene + %.0f" % (a[0], a[1]))
+            last = np.argsort(end)[-8:]
+            for i in last:
+                print("   late wave %6d wg %5d start %6d ph1 %6d ph2 %6d chunks %3d genes %3d" % (
+                    idx[i], idx[i] // 8, start[i], ph1[i], ph2[i], t[i, 5], t[i, 4]))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -92,7 +92,8 @@ struct KT {
   static constexpr int IMG = 8 * TR;              // one chunk: th_u rows of obs 0-3, th_v rows
   static constexpr int SW = (K % 2 == 0) ? 2 : 1;  // staging width: double2 pieces when K is even
   static constexpr int NPC = (8 * KP / SW + 63) / 64;  // staged pieces per lane per chunk
-  static constexpr int IMG_BYTES = NW * 2 * IMG * 8;
+  static constexpr int IMGW = 2 * IMG + 2;        // per wave: double buffer + a dummy piece slot
+  static constexpr int IMG_BYTES = NW * IMGW * 8;
   static constexpr int GMAX_RAW = (lds_target(K) - IMG_BYTES - 64) / ((VDBL + KP) * 8);
   static constexpr int GMAX = GMAX_RAW > 64 ? 64 : (GMAX_RAW < 4 ? 4 : GMAX_RAW);
   static constexpr int LDS_A = GMAX * VDBL * 8 + GMAX * KP * 8 + IMG_BYTES + 64;
@@ -111,6 +112,18 @@ int gmax_for(int K);  // host view of KT<K>::GMAX (table below)
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// Stores of the per-iteration intermediates (c, partial rows, S partials, the p snapshot) write
+// through the XCD L2 (agent-scope relaxed atomic store = global_store sc1): their bytes leave L2
+// while the kernel runs instead of being written back at the kernel boundary.  -DMMSBM_WT=0
+// builds plain stores (measurement).
+#ifndef MMSBM_WT
+#define MMSBM_WT 1
+#endif
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  if constexpr (MMSBM_WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -134,7 +147,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define MMSBM_STAMP 0
 #endif
 __device__ unsigned long long* g_stamp = nullptr;
-constexpr int STAMP_SLOTS = 6;
+constexpr int STAMP_SLOTS = 8;
 constexpr long long STAMP_WAVES = 1 << 16;  // per kernel id
 struct Stamp {
   unsigned long long t[STAMP_SLOTS];
@@ -180,7 +193,7 @@ template <int K>
 __device__ __forceinline__ void s_partial(const double* __restrict__ th, const double* __restrict__ prows_b,
                                           const int* __restrict__ prow_gene, int q0, int q1,
                                           double* __restrict__ out, double* __restrict__ Tq, int ig,
-                                          int tid, int wv, int hi, int blk, int lo) {
+                                          int tid, int wv, int hi, int blk, int lo, Stamp& st_) {
   using T = KT<K>;
   // blocks of QB partial rows: their genes' theta rows staged in LDS (zero padded), so the loop
   // over the block only streams the partial rows themselves from HBM
@@ -203,6 +216,7 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
     for (int i = 0; i < NI; ++i)
       if (tid + NT * i < QB * T::KP) Tq[tid + NT * i] = x[i];
     __syncthreads();
+    st_.mark(1);
     for (int qq = 0; qq < nq; qq += 16) {  // 4 MFMA steps per round, their loads issued together
       double m[4][T::NSI];
 #pragma unroll
@@ -237,9 +251,10 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
     if (it < T::NG * T::NCG) {
       const int at = it / T::NCG, cg = it % T::NCG;
       const int a = 4 * at + hi, cell = 4 * (4 * cg + blk) + lo;
-      if (a < K && cell < T::K2) out[(size_t)a * T::K2 + cell] = acc[k];
+      if (a < K && cell < T::K2) st_wt(out + (size_t)a * T::K2 + cell, acc[k]);
     }
   }
+  st_.mark(2);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -278,13 +293,11 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       const int sw = w - n_wg, sp = sw / T::NIG, ig = sw % T::NIG;
       const int* d = sp_desc + 3 * sp;
       s_partial<K>(th, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
-                   spart + ((size_t)b * n_sp + sp) * T::K3, smem, ig, tid, wv, hi, blk, lo);
+                   spart + ((size_t)b * n_sp + sp) * T::K3, smem, ig, tid, wv, hi, blk, lo, st_);
       const long long tot = (long long)R * T::K3, nsw = (long long)n_sp * T::NIG;
       const long long c0 = tot * sw / nsw, c1 = tot * (sw + 1) / nsw;
       for (long long idx = c0 + tid; idx < c1; idx += NT)
-        pold[(size_t)b * tot + idx] = pr[(size_t)b * tot + idx];
-      st_.mark(1);
-      st_.mark(2);
+        st_wt(pold + (size_t)b * tot + idx, pr[(size_t)b * tot + idx]);
       st_.mark(3);
       st_.flush(3, wave_id, lane);
       return;
@@ -296,7 +309,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   const double* __restrict__ p = pr + ((size_t)b * R + r) * T::K3;
   double* Vt = smem;
   double* Tg = smem + (MODE == PASS_B ? 0 : T::GMAX * T::VDBL);  // theta rows of the V genes
-  double* img = smem + (MODE == PASS_B ? 0 : T::GMAX * (T::VDBL + T::KP)) + wv * 2 * T::IMG;
+  double* img = smem + (MODE == PASS_B ? 0 : T::GMAX * (T::VDBL + T::KP)) + wv * T::IMGW;
 
   // this wave's unit, and the first records of its pipeline (in flight during the V prologue).
   // Record stream: lane l < 16 holds int l of the chunk's 4 records (i, j, k, w), lane 16 the
@@ -304,17 +317,17 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   // no register array is indexed at run time.
   // Ring of U record registers: the loop below is unrolled U times so each ring slot keeps a
   // fixed register (a rotation by register moves would wait for every load in flight).
-  constexpr int U = 6;   // records U - 1 chunks ahead; theta values and c two ahead (ring of 3)
+  constexpr int U = 6;   // records U - 1 chunks ahead
+  constexpr int DT = 2;  // theta values and c DT chunks ahead (ring of U slots, DT + 1 live)
   const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
   const int* __restrict__ rows_i = reinterpret_cast<const int*>(rows);
   // Every load in the chunk loop is issued by every lane on every path (addresses clamped, values
   // selected afterwards): an exec-masked load behind a branch would make the compiler's vmcnt
   // accounting assume it may be missing and wait for everything in flight.
-  auto ld_rec = [&](int q) -> int {
-    const int l = lane & 31;
-    const int* src = l < 16 ? rows_i + (size_t)q * 16 + l : l == 16 ? chunk_prow + q : chunk_vslot + q;
-    return *src;
-  };
+  const int lr = lane & 31;  // this lane's record word: base and stride fixed once
+  const int* __restrict__ rbase = lr < 16 ? rows_i + lr : lr == 16 ? chunk_prow : chunk_vslot;
+  const int rstride = lr < 16 ? 16 : 1;
+  auto ld_rec = [&](int q) -> int { return rbase[(size_t)q * rstride]; };
   auto clampq = [&](int q) { return q < c1 ? q : c1 - 1; };
   const bool any = c0 < c1;
   int rv[U];
@@ -324,24 +337,50 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 
   if constexpr (MODE != PASS_B) {
     // ---- V_g[b][h] = sum_a th_g[a] p_r[a][b][h] for the workgroup's pivot genes (LDS)
-    const int gb = wg_gene[w], ng = wg_gene[w + 1] - gb;
+    // vgenes holds GMAX (padded) genes per workgroup, so the theta loads do not wait for
+    // wg_gene; p_r is staged in the image region when it fits.  All loads go out together.
+    const int ng = wg_gene[w + 1] - wg_gene[w];
+    const int* __restrict__ vgw = vgenes + (size_t)w * T::GMAX;
+    constexpr bool PV = T::K3 <= NW * T::IMGW;
+    double* Ps = smem + T::GMAX * (T::VDBL + T::KP);
+    constexpr int NTG = (T::GMAX * T::KP + NT - 1) / NT, NPV = PV ? (T::K3 + NT - 1) / NT : 1;
+    double tg[NTG], pv[NPV];
+#pragma unroll
+    for (int i = 0; i < NTG; ++i) {
+      const int idx = tid + NT * i, gl = idx / T::KP, a = idx % T::KP;
+      const int g = vgw[gl < T::GMAX ? gl : 0];
+      tg[i] = th[(size_t)g * K + (a < K ? a : 0)];
+    }
+    if constexpr (PV) {
+#pragma unroll
+      for (int i = 0; i < NPV; ++i) pv[i] = p[tid + NT * i < T::K3 ? tid + NT * i : 0];
+    }
     constexpr int ZR = (T::VROWS - K) * VR;  // rows b >= K read as zero
     if constexpr (ZR > 0)
       for (int idx = tid; idx < ng * ZR; idx += NT)
         Vt[(idx / ZR) * T::VDBL + K * VR + idx % ZR] = 0.0;
-    for (int idx = tid; idx < ((ng + 3) & ~3) * T::KP; idx += NT) {  // theta rows, zero padded
-      const int gl = idx / T::KP, a = idx % T::KP;
-      Tg[idx] = (gl < ng && a < K) ? th[(size_t)vgenes[gb + gl] * K + a] : 0.0;
+#pragma unroll
+    for (int i = 0; i < NTG; ++i) {  // theta rows, zero padded
+      const int idx = tid + NT * i, gl = idx / T::KP, a = idx % T::KP;
+      if (idx < T::GMAX * T::KP) Tg[idx] = (gl < ng && a < K) ? tg[i] : 0.0;
     }
+    if constexpr (PV) {
+#pragma unroll
+      for (int i = 0; i < NPV; ++i)
+        if (tid + NT * i < T::K3) Ps[tid + NT * i] = pv[i];
+    }
+    const double* __restrict__ pv_src = PV ? Ps : p;
     __syncthreads();
+    st_.mark(6);
     constexpr int CT = K * NG;  // (b, h tile) cell tiles
     constexpr int CG = (CT + 3) / 4;
     const int GT = (ng + 3) / 4;
-    // items (gene tile, 4 cell tiles); two per round so their p loads go out together
-    for (int i0 = wv; i0 < GT * CG; i0 += 2 * NW) {
-      double av[2][NG], bv[2][NG];
+    // items (gene tile, 4 cell tiles); IPR per round: independent MFMA chains, reads together
+    constexpr int IPR = 2;
+    for (int i0 = wv; i0 < GT * CG; i0 += IPR * NW) {
+      double av[IPR][NG], bv[IPR][NG];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < IPR; ++u) {
         const int item = i0 + u * NW;
         const bool iv = item < GT * CG;
         const int gt = iv ? item / CG : 0, cg = iv ? item % CG : 0;
@@ -352,11 +391,11 @@ __global__ __launch_bounds__(NT) void pass_kernel(
         for (int as = 0; as < NG; ++as) {
           const int a = 4 * as + hi;
           av[u][as] = Tg[(4 * gt + lo) * T::KP + a];
-          bv[u][as] = (cv && a < K && hh < K) ? p[(a * K + bb) * K + hh] : 0.0;
+          bv[u][as] = (cv && a < K && hh < K) ? pv_src[(a * K + bb) * K + hh] : 0.0;
         }
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < IPR; ++u) {
         const int item = i0 + u * NW;
         double acc = 0.0;
 #pragma unroll
@@ -379,26 +418,32 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   const int ucomp = s == 0 ? 1 : 0, vcomp = s == 2 ? 1 : 2;
   // staged pieces of one chunk: piece pc = 64 t + lane is SW doubles of row8 = pc / (KP / SW)
   // (rows 0-3: th_u of obs 0-3, rows 4-7: th_v), columns SW (pc % (KP / SW)) ..
-  using SV = typename std::conditional<T::SW == 2, double2, double>::type;
+  typedef double d2v __attribute__((ext_vector_type(2)));  // a native vector: SROA-friendly
+  using SV = typename std::conditional<T::SW == 2, d2v, double>::type;
   constexpr int PR = T::KP / T::SW;  // pieces per image row
+  // A piece outside the image (lanes past 8 PR) or in the zero pad columns is still loaded (from
+  // a clamped address) and stored, to a per-wave dummy slot: no select, so the load cannot be
+  // sunk behind an exec mask.
+  double* dummy = img + 2 * T::IMG;
+  int soff[T::NPC];  // image offset of each piece, or -1 for the dummy slot
+#pragma unroll
+  for (int t = 0; t < T::NPC; ++t) {
+    const int pc = 64 * t + lane, col = T::SW * (pc % PR);
+    soff[t] = (pc < 8 * PR && col < K) ? (pc / PR) * TR + col : -1;
+  }
   auto stage_load = [&](int rv, SV (&v)[T::NPC]) {
 #pragma unroll
     for (int t = 0; t < T::NPC; ++t) {
       const int pc = 64 * t + lane;
       const int row8 = pc < 8 * PR ? pc / PR : 0, col = T::SW * (pc % PR);
       const int g = __shfl(rv, (row8 & 3) * 4 + ((row8 >> 2) ? vcomp : ucomp), 64);
-      const bool ok = pc < 8 * PR && col < K;
-      const SV x = *reinterpret_cast<const SV*>(th + (size_t)g * K + (col < K ? col : K - T::SW));
-      if constexpr (T::SW == 2) v[t] = ok ? x : make_double2(0.0, 0.0);
-      else v[t] = ok ? x : 0.0;
+      v[t] = *reinterpret_cast<const SV*>(th + (size_t)g * K + (col < K ? col : K - T::SW));
     }
   };
   auto stage_store = [&](double* I, const SV (&v)[T::NPC]) {
 #pragma unroll
-    for (int t = 0; t < T::NPC; ++t) {
-      const int pc = 64 * t + lane;
-      if (pc < 8 * PR) *reinterpret_cast<SV*>(I + (pc / PR) * TR + T::SW * (pc % PR)) = v[t];
-    }
+    for (int t = 0; t < T::NPC; ++t)
+      *reinterpret_cast<SV*>(soff[t] >= 0 ? I + soff[t] : dummy) = v[t];
   };
 
   double macc[T::NTS];
@@ -412,15 +457,14 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   // w of observation hi (count on stream 0, c index on streams 1 / 2) of a record register
   auto rec_w = [&](int r) { return __shfl(r, hi * 4 + 3, 64); };
   if (any) {
-    // Software pipeline: records U - 1 chunks ahead, theta values (and c) two ahead; the LDS
+    // Software pipeline: records U - 1 chunks ahead, theta values (and c) DT ahead; the LDS
     // image of chunk q + 1 is written at the end of chunk q (double buffer).
-    SV st[3][T::NPC];  // theta values of chunk q in slot (q - c0) % 3
-    double cr[3] = {0.0, 0.0, 0.0};  // PASS_B: c of observation hi, same slots
-    stage_load(rv[0], st[0]);
-    stage_load(rv[1], st[1]);
-    if constexpr (MODE == PASS_B) {
-      cr[0] = cb[rec_w(rv[0])];
-      cr[1] = cb[rec_w(rv[1])];
+    SV st[U][T::NPC];  // theta values of chunk q in slot (q - c0) % U
+    double cr[U];      // PASS_B: c of observation hi, same slots
+#pragma unroll
+    for (int i = 0; i < DT; ++i) {
+      stage_load(rv[i], st[i]);
+      if constexpr (MODE == PASS_B) cr[i] = cb[rec_w(rv[i])];
     }
     stage_store(img, st[0]);
     for (int q0 = c0; q0 < c1; q0 += U) {
@@ -429,17 +473,17 @@ __global__ __launch_bounds__(NT) void pass_kernel(
         const int q = q0 + ph;
         if (q >= c1) break;
         const int buf = ph & 1;  // U is even: the image buffer alternates with q
-        // prefetch: records of chunk q + U - 1 into the slot chunk q - 1 used, theta / c of q + 2
+        // prefetch: records of chunk q + U - 1 into the slot chunk q - 1 used, theta / c of q + DT
         rv[(ph + U - 1) % U] = ld_rec(clampq(q + U - 1));
-        stage_load(rv[(ph + 2) % U], st[(ph + 2) % 3]);
-        if constexpr (MODE == PASS_B) cr[(ph + 2) % 3] = cb[rec_w(rv[(ph + 2) % U])];
+        stage_load(rv[(ph + DT) % U], st[(ph + DT) % U]);
+        if constexpr (MODE == PASS_B) cr[(ph + DT) % U] = cb[rec_w(rv[(ph + DT) % U])];
         wave_lds_sync();
         const double* I = img + buf * T::IMG;
         const int rq = rv[ph % U];
         const int pr0 = __builtin_amdgcn_readlane(rq, 16);
         const int pr1 = __builtin_amdgcn_readlane(rv[(ph + 1) % U], 16);
 
-        double c = cr[ph % 3];
+        double c = MODE == PASS_B ? cr[ph] : 0.0;
         if constexpr (MODE != PASS_B) {
           // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
           const int nw = rec_w(rq);
@@ -461,7 +505,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
             if ((lane & 15) == 0) ll += (double)nw * log(d);
           } else {
             c = (double)nw / d;
-            cb[(size_t)q * CH + hi] = c;  // the 16 lanes of row hi store the same value
+            st_wt(cb + (size_t)q * CH + hi, c);  // the 16 lanes of row hi store the same value
           }
         }
         if constexpr (MODE != PASS_LL) {
@@ -484,19 +528,20 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 #pragma unroll
             for (int ts = 0; ts < T::NTS; ++ts) {
               const int x = 4 * (ts / T::NGB) + hi, y = 4 * (4 * (ts % T::NGB) + blk) + lo;
-              if (x < K && y < K) out[x * K + y] = macc[ts];
+              if (x < K && y < K) st_wt(out + x * K + y, macc[ts]);
               macc[ts] = 0.0;
             }
           }
         }
         // next chunk's image into the other buffer (its reads of this buffer are done)
         wave_lds_sync();
-        stage_store(img + (buf ^ 1) * T::IMG, st[(ph + 1) % 3]);
+        stage_store(img + (buf ^ 1) * T::IMG, st[(ph + 1) % U]);
       }
     }
   }
   st_.mark(2);
   st_.t[5] = (unsigned long long)(c1 - c0);
+  if constexpr (MODE != PASS_B) st_.t[4] = (unsigned long long)(wg_gene[w + 1] - wg_gene[w]);
   if constexpr (MODE == PASS_LL) {
     // fixed-order workgroup sum of the log-likelihood terms
     __shared__ double red[NW];
@@ -633,13 +678,16 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
       const int ncb = NC - cb0 < F::CB ? NC - cb0 : F::CB;
       const int NE = ncb * 4 * F::K2P;
       __syncthreads();
-      // Ms[c][gene][k] = the gene's partial rows summed in row order; eight entries per thread
-      // per round, their first two rows loaded together (addresses clamped, loads unconditional)
-      for (int i0 = tid; i0 < NE; i0 += 8 * FIN_NT) {
-        int qa[8], qb[8], kk[8];
-        double v1[8], v2[8];
+      st_.mark(4);
+      // Ms[c][gene][k] = the gene's partial rows summed in row order; RE entries per thread per
+      // round (one round for K <= 12), their first two rows loaded together (addresses clamped,
+      // loads unconditional)
+      constexpr int NEPT = (F::CB * 4 * F::K2P + FIN_NT - 1) / FIN_NT, RE = NEPT < 12 ? NEPT : 12;
+      for (int i0 = tid; i0 < NE; i0 += RE * FIN_NT) {
+        int qa[RE], qb[RE], kk[RE];
+        double v1[RE], v2[RE];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < RE; ++u) {
           const int idx = i0 + u * FIN_NT;
           const int c = idx / (4 * F::K2P), rem = idx % (4 * F::K2P);
           const int gl = rem / F::K2P, k = rem % F::K2P;
@@ -651,13 +699,14 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
           v2[u] = pb[(size_t)(qa[u] + 1 < qb[u] ? qa[u] + 1 : 0) * K2 + kk[u]];
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < RE; ++u) {
           const int idx = i0 + u * FIN_NT;
           double m = qa[u] < qb[u] ? v1[u] : 0.0;
           if (qa[u] + 1 < qb[u]) m += v2[u];
           for (int q = qa[u] + 2; q < qb[u]; ++q) m += pb[(size_t)q * K2 + kk[u]];
           if (idx < NE) Ms[idx] = m;
         }
+        st_.mark(5);
       }
       __syncthreads();
       st_.mark(1);
@@ -1164,7 +1213,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   const bool em = which == MMSBM_SET_TRAIN;
   // unit counts do not depend on B, so a sample's sums (and its bits) are the same whatever its
   // batch; MMSBM_UNITS="a,b" overrides them (tests: tiny units force every split path)
-  int units_a = 3072, units_b = 6144;
+  int units_a = 1536, units_b = 3072;
   if (const char* u = getenv("MMSBM_UNITS")) {
     int a = 0, b = 0;
     if (sscanf(u, "%d,%d", &a, &b) == 2 && a > 0 && b > 0) {
@@ -1181,7 +1230,17 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   if ((rc = upload(&sd.wg_units, h.wg_units))) return rc;
   if ((rc = upload(&sd.wg_code, h.wg_code))) return rc;
   if ((rc = upload(&sd.wg_gene, h.wg_gene))) return rc;
-  if ((rc = upload(&sd.vgenes, h.vgenes))) return rc;
+  {  // pivot genes padded to GMAX per stream-0 workgroup (the pass prologue indexes w GMAX + slot)
+    const int gm = gmax_for(c->K);
+    const size_t nw = h.wg_gene.empty() ? 0 : h.wg_gene.size() - 1;
+    std::vector<int> vpad(std::max<size_t>(nw * gm, 1), 0);
+    for (size_t w = 0; w < nw; ++w) {
+      const int g0 = h.wg_gene[w], ng = h.wg_gene[w + 1] - g0;
+      if (ng > gm) return fail(MMSBM_ERR_INVALID, "plan: %d genes in a workgroup (max %d)", ng, gm);
+      for (int i = 0; i < gm; ++i) vpad[w * gm + i] = ng ? h.vgenes[g0 + (i < ng ? i : ng - 1)] : 0;
+    }
+    if ((rc = upload(&sd.vgenes, vpad))) return rc;
+  }
   if ((rc = upload(&sd.prow_ptr, h.prow_ptr))) return rc;
   if ((rc = upload(&sd.prow_gene, h.prow_gene))) return rc;
   if ((rc = upload(&sd.sp_desc, h.sp_desc))) return rc;
@@ -1267,6 +1326,12 @@ int mmsbm_iterate(mmsbm_ctx* c, double* theta, double* pr, int32_t n_iters, void
     std::vector<unsigned long long> h((size_t)5 * STAMP_WAVES * STAMP_SLOTS);
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipMemcpy(h.data(), c->stamp, h.size() * 8, hipMemcpyDeviceToHost));
+    if (const char* path = getenv("MMSBM_STAMP_DUMP")) {  // raw [kernel][wave][slot] words
+      if (FILE* f = fopen(path, "wb")) {
+        fwrite(h.data(), 8, h.size(), f);
+        fclose(f);
+      }
+    }
     const char* names[5] = {"passA", "passB", "fin", "spart", "passLL"};
     for (int k = 0; k < 5; ++k) {
       double sum[4] = {0, 0, 0, 0}, chunks = 0;

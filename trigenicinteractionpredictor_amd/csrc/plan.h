@@ -283,7 +283,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       const int q1 = pl.prow_ptr[(size_t)r * (P + 1) + P];
       pl.sp_lo[r] = pl.n_sp;
       const int n = q1 - q0;
-      const int parts = n <= 0 ? 0 : std::min(256, std::max(1, n / 32));
+      const int parts = n <= 0 ? 0 : std::min(256, std::max(1, n / 16));
       for (int k = 0; k < parts; ++k) {
         pl.sp_desc.push_back(r);
         pl.sp_desc.push_back(q0 + (int)((long long)n * k / parts));
