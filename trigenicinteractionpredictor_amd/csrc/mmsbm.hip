@@ -576,16 +576,27 @@ struct SpRange {
 
 template <int K>
 struct FT {
-  static constexpr int K2 = K * K, NG = (K + 3) / 4;
+  static constexpr int K2 = K * K, NG = (K + 3) / 4, KP = 4 * NG;
   static constexpr int KS = (K2 + 3) / 4;       // k-steps over the dense (y, z) cells
   static constexpr int K2P = 4 * KS;
   static constexpr int NXG = (NG + 3) / 4;      // MFMA groups of 4 x tiles
+  // K <= 12: 4 genes per workgroup of 4 waves, p of every rating staged in LDS.  K > 12: 16 genes
+  // (4 MFMA row tiles sharing each p load) per workgroup of 8 waves, one combo at a time in LDS.
+  static constexpr int GT = K <= 12 ? 1 : 4;
+  static constexpr int NGW = 4 * GT;
+  static constexpr int NT = GT == 1 ? 256 : 512;
+  static constexpr int NPART = NT / 64;         // cell part: threads per cell
+  static constexpr int KSPLIT = GT == 1 ? 1 : 8 / NXG;  // big: k-step parts over the 8 waves
   static constexpr int CB_RAW = (60 * 1024) / (4 * K2P * 8);
-  static constexpr int CB = CB_RAW > 6 ? 6 : (CB_RAW < 1 ? 1 : CB_RAW);  // combos staged at once
-  static constexpr int MS_G = CB * 4 * K2P > 4 * NXG * 64 ? CB * 4 * K2P : 4 * NXG * 64;
-  static constexpr int MS = MS_G > MAX_R * 4 * 64 ? MS_G : MAX_R * 4 * 64;  // doubles
+  static constexpr int CB = GT > 1 ? 1 : (CB_RAW > 6 ? 6 : (CB_RAW < 1 ? 1 : CB_RAW));
+  static constexpr int MS_G = GT > 1 ? NGW * K2P + KSPLIT * NGW * KP
+                                     : (CB * 4 * K2P > 4 * NXG * 64 ? CB * 4 * K2P : 4 * NXG * 64);
+  static constexpr int MS = MS_G > MAX_R * NPART * 64 ? MS_G : MAX_R * NPART * 64;  // doubles
   static constexpr bool PLDS = K <= 12;  // p of every rating staged in LDS (else read from L2)
   static constexpr int LDS = (MS + (PLDS ? MAX_R * K * K * K : 0)) * 8;
+  static_assert(GT == 1 || NXG * KSPLIT == 8, "big fin: one (x group, k part) per wave");
+  static_assert(GT == 1 || NGW * K <= NT, "big fin epilogue: one (gene, x) per thread");
+  static_assert(LDS <= 160 * 1024, "fin LDS over budget");
 };
 
 // One (combo, x group) item of the fin gene part: sum_k M_g[k] P^s[k][x] over the dense (y, z)
@@ -621,8 +632,135 @@ __device__ __forceinline__ double x_item(const double* __restrict__ Mg, const do
   return a2;
 }
 
+// The same contraction for GT gene tiles at once (big fin): each p load feeds GT MFMAs, over the
+// k-steps [kb, ke).  Mg = tile 0's row of lane lo; tile t's row is Mg + 4 t K2P.
+template <int K, int S>
+__device__ __forceinline__ void x_tiles(const double* __restrict__ Mg, const double* __restrict__ p,
+                                        int x, int hi, int kb, int ke, double (&acc)[FT<K>::GT]) {
+  using F = FT<K>;
+  constexpr int K2 = K * K, UB = 8, GT = F::GT;
+  const int xc = x < K ? x : K - 1;
+#pragma unroll 1
+  for (int ks0 = kb; ks0 < ke; ks0 += UB) {
+    double bv[UB];
+    int kk[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int ks = ks0 + u < ke ? ks0 + u : ke - 1;
+      const int k = 4 * ks + hi, kc = k < K2 ? k : K2 - 1;
+      int idx;
+      if constexpr (S == 0) idx = xc * K2 + kc;
+      else if constexpr (S == 2) idx = kc * K + xc;
+      else idx = kc + (kc / K) * (K2 - K) + xc * K;
+      bv[u] = p[idx];
+      kk[u] = k;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const bool ok = ks0 + u < ke;
+#pragma unroll
+      for (int t = 0; t < GT; ++t) {
+        const double m = Mg[t * 4 * F::K2P + kk[u]];
+        acc[t] = mfma4(ok ? m : 0.0, bv[u], acc[t]);
+      }
+    }
+  }
+}
+
+// Gene part of fin_kernel for K > 12: 16 genes per workgroup (4 MFMA row tiles), 8 waves.  For
+// each combo (s, r) in order, the 16 genes' partial rows are summed into LDS; wave w then takes
+// x group w % NXG and k-step part w / NXG of all 4 gene tiles, so each p load feeds 4 MFMAs.
+// The k parts are added in order in the epilogue.
 template <int K, bool SUMS>
-__global__ __launch_bounds__(FIN_NT) void fin_kernel(
+__device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const double* __restrict__ pold,
+                                              const double* __restrict__ prows,
+                                              const int* __restrict__ prow_ptr, const int* __restrict__ deg,
+                                              int P, int R, long long n_prows, double* __restrict__ nth_out,
+                                              double* Ms, Stamp& st_) {
+  using F = FT<K>;
+  constexpr int K2 = F::K2, K3 = K * K * K, NGW = F::NGW, NT = F::NT, KP = F::KP;
+  const int tid = threadIdx.x, b = blockIdx.y;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
+  const int g0 = blockIdx.x * NGW;
+  const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
+  const int NC = 3 * R;
+  double* Xr = Ms + NGW * F::K2P;  // [KSPLIT][NGW][KP]
+  // epilogue operands (thread t < NGW K: gene g0 + t / K, x = t % K), loaded up front
+  const int eg = tid / K, ex = tid % K;
+  const int ge = g0 + eg < P ? g0 + eg : P - 1;
+  const double th_e = theta[((size_t)b * P + ge) * K + ex];
+  const int deg_e = deg[ge];
+  __shared__ int pp[3 * MAX_R][NGW + 1];
+  {
+    const int c = tid / (NGW + 1), i = tid % (NGW + 1);
+    const int v = prow_ptr[(size_t)(c < NC ? c : 0) * (P + 1) + (g0 + i < P ? g0 + i : P)];
+    if (c < NC) pp[c][i] = v;
+  }
+  const int xg = wv % F::NXG, ksp = wv / F::NXG;
+  const int kb = F::KS * ksp / F::KSPLIT, ke = F::KS * (ksp + 1) / F::KSPLIT;
+  const int x = 4 * (4 * xg + blk) + lo;
+  double acc[F::GT];
+#pragma unroll
+  for (int t = 0; t < F::GT; ++t) acc[t] = 0.0;
+  constexpr int NE = NGW * F::K2P;
+  constexpr int NEPT = (NE + NT - 1) / NT, RE = NEPT < 12 ? NEPT : 12;
+  for (int combo = 0; combo < NC; ++combo) {
+    __syncthreads();
+    st_.mark(4);
+    for (int i0 = tid; i0 < NE; i0 += RE * NT) {
+      int qa[RE], qb[RE], kk[RE];
+      double v1[RE], v2[RE];
+#pragma unroll
+      for (int u = 0; u < RE; ++u) {
+        const int idx = i0 + u * NT;
+        const int gl = idx / F::K2P, k = idx % F::K2P;
+        const bool ok = idx < NE && k < K2;
+        qa[u] = ok ? pp[combo][gl] : 0;
+        qb[u] = ok ? pp[combo][gl + 1] : 0;
+        kk[u] = k < K2 ? k : 0;
+        v1[u] = pb[(size_t)(qa[u] < qb[u] ? qa[u] : 0) * K2 + kk[u]];
+        v2[u] = pb[(size_t)(qa[u] + 1 < qb[u] ? qa[u] + 1 : 0) * K2 + kk[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < RE; ++u) {
+        const int idx = i0 + u * NT;
+        double m = qa[u] < qb[u] ? v1[u] : 0.0;
+        if (qa[u] + 1 < qb[u]) m += v2[u];
+        for (int q = qa[u] + 2; q < qb[u]; ++q) m += pb[(size_t)q * K2 + kk[u]];
+        if (idx < NE) Ms[idx] = m;
+      }
+      st_.mark(5);
+    }
+    __syncthreads();
+    st_.mark(1);
+    const int s = combo / R, r = combo % R;
+    const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
+    const double* __restrict__ Mg = Ms + (size_t)lo * F::K2P;
+    if (s == 0) x_tiles<K, 0>(Mg, p, x, hi, kb, ke, acc);
+    else if (s == 1) x_tiles<K, 1>(Mg, p, x, hi, kb, ke, acc);
+    else x_tiles<K, 2>(Mg, p, x, hi, kb, ke, acc);
+  }
+  st_.mark(2);
+  // X[gene 4 t + hi][x]: the k parts added in order
+#pragma unroll
+  for (int t = 0; t < F::GT; ++t)
+    if (x < K) Xr[(ksp * NGW + 4 * t + hi) * KP + x] = acc[t];
+  __syncthreads();
+  if (tid < NGW * K && g0 + eg < P) {
+    double X = Xr[eg * KP + ex];
+#pragma unroll
+    for (int q = 1; q < F::KSPLIT; ++q) X += Xr[(q * NGW + eg) * KP + ex];
+    const size_t o = ((size_t)b * P + g0 + eg) * K + ex;
+    if constexpr (SUMS) nth_out[o] = X;
+    else theta[o] = th_e * X / (double)deg_e;
+  }
+  st_.mark(3);
+  st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 8 + wv, lane);
+}
+
+template <int K, bool SUMS>
+__global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
     double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ pold,
     const double* __restrict__ prows, const int* __restrict__ prow_ptr,
     const double* __restrict__ spart, const int* __restrict__ deg, SpRange spr, int P, int R,
@@ -634,7 +772,13 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
   const int tid = threadIdx.x, b = blockIdx.y;
   Stamp st_{};
   st_.mark(0);
-  if ((int)blockIdx.x < n_gene_wg) {
+  if constexpr (F::GT > 1) {
+    if ((int)blockIdx.x < n_gene_wg) {
+      fin_genes_big<K, SUMS>(theta, pold, prows, prow_ptr, deg, P, R, n_prows, nth_out, Ms, st_);
+      return;
+    }
+  }
+  if (F::GT == 1 && (int)blockIdx.x < n_gene_wg) {
     const int lane = tid & 63, wv = tid >> 6;
     const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
     const int g0 = blockIdx.x * 4;
@@ -746,8 +890,9 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
     st_.mark(3);
     st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 4 + wv, lane);
   } else {
-    // 64 cells per workgroup, four threads per cell, each summing a quarter of every rating's S
-    // partials (16 loads in flight), the quarters combined in order through LDS
+    // 64 cells per workgroup, NPART threads per cell, each summing a share of every rating's S
+    // partials (16 loads in flight), the shares combined in order through LDS
+    constexpr int NPART = F::NPART;
     const int cl = tid & 63, part = tid >> 6;
     const int cell = (blockIdx.x - n_gene_wg) * 64 + cl;
     const bool cv = cell < K3;
@@ -757,7 +902,7 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
     for (int r = 0; r < MAX_R; ++r) po[r] = pold[((size_t)b * R + (r < R ? r : R - 1)) * K3 + cc];
     for (int r = 0; r < R; ++r) {
       const int n = spr.hi[r] - spr.lo[r];
-      const int s0 = spr.lo[r] + n * part / 4, s1 = spr.lo[r] + n * (part + 1) / 4;
+      const int s0 = spr.lo[r] + n * part / NPART, s1 = spr.lo[r] + n * (part + 1) / NPART;
       double S = 0.0;
       for (int sp = s0; sp < s1; sp += 16) {
         double v[16];
@@ -769,7 +914,7 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
 #pragma unroll
         for (int u = 0; u < 16; ++u) S += v[u];
       }
-      Ms[(r * 4 + part) * 64 + cl] = S;
+      Ms[(r * NPART + part) * 64 + cl] = S;
     }
     __syncthreads();
     if (part == 0 && cv) {
@@ -778,8 +923,9 @@ __global__ __launch_bounds__(FIN_NT) void fin_kernel(
 #pragma unroll
       for (int r = 0; r < MAX_R; ++r) {
         if (r < R) {
-          const double S = ((Ms[r * 256 + cl] + Ms[r * 256 + 64 + cl]) + Ms[r * 256 + 128 + cl]) +
-                           Ms[r * 256 + 192 + cl];
+          double S = Ms[r * NPART * 64 + cl];
+#pragma unroll
+          for (int q = 1; q < NPART; ++q) S += Ms[(r * NPART + q) * 64 + cl];
           if constexpr (SUMS) {
             S_out[((size_t)b * R + r) * K3 + cell] = S;
           } else {
@@ -1036,7 +1182,7 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   using T = KT<K>;
   const SetDev& sd = c->sets[MMSBM_SET_TRAIN];
   const auto& h = sd.h;
-  const int ngw = (c->P + 3) / 4;
+  const int ngw = (c->P + FT<K>::NGW - 1) / FT<K>::NGW;
   const int ncw = (T::K3 + 63) / 64;
   int rc;
   if ((rc = lds_opt_in(c, sums ? 3 : 2, sums ? &fin_kernel<K, true> : &fin_kernel<K, false>, FT<K>::LDS)))
@@ -1048,11 +1194,11 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
     spr.hi[r] = h.sp_hi[r];
   }
   if (sums)
-    fin_kernel<K, true><<<dim3(ngw + ncw, c->B), FIN_NT, lds, s>>>(
+    fin_kernel<K, true><<<dim3(ngw + ncw, c->B), FT<K>::NT, lds, s>>>(
         theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_sp, 1), ngw, c->eps, nth, S);
   else
-    fin_kernel<K, false><<<dim3(ngw + ncw, c->B), FIN_NT, lds, s>>>(
+    fin_kernel<K, false><<<dim3(ngw + ncw, c->B), FT<K>::NT, lds, s>>>(
         theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_sp, 1), ngw, c->eps, nth, S);
   HIP_TRY(hipGetLastError());

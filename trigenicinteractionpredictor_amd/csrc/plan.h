@@ -131,8 +131,12 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       }
       (s == 0 ? chunks_a : chunks_b) += nch;
     }
-  const int lmax_a = (int)std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1));
-  const int lmax_b = (int)std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1));
+  // unit length: the work spread over about units_* units, but no unit longer than LCAP chunks
+  // (large link sets get more units rather than longer ones, so a few long units do not set
+  // the kernel's duration)
+  constexpr long long LCAP = 64;
+  const int lmax_a = (int)std::min(LCAP, std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1)));
+  const int lmax_b = (int)std::min(LCAP, std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1)));
 
   std::vector<int> wg_stream;
   for (int s = 0; s < pl.streams; ++s) {
