@@ -1,6 +1,6 @@
 """Instruction mix of one kernel in a hipcc -S device assembly file (measurement aid).
 
-    python tools/isa_stats.py /tmp/mmsbm.s emx_kernelILi10 [--dump out.s]
+    python tools/isa_stats.py /tmp/mmsbm.s pass_kernelILi10ELi0E [--dump out.s]
 """
 import re
 import sys

@@ -1,0 +1,35 @@
+"""profiles/pmc_r02_K<K>.json from a tools/gpu_r02_prof.sh output directory: HBM bytes per launch
+of each kernel of the iteration = 2 x FETCH_SIZE (gfx950: FETCH_SIZE tallies 128-B requests at
+64 B, MI355X_MICROARCH.md) + WRITE_SIZE, both in KiB per dispatch, averaged over the dispatches
+of the PMC passes.  usage: python tools/pmc_to_traffic.py gpurun_out/<tag> K E_obs B out.json"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+NAMES = {"pass_kernel<%d, 0>": "pass_a", "pass_kernel<%d, 2>": "pass_b", "fin_kernel<%d, false>": "fin"}
+
+
+def main(root, K, E_obs, B, out):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(root + "/p*/run_counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            k = row["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+            acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    rec = {"K": K, "E_obs": E_obs, "B": B, "source": root, "hbm_bytes_per_launch": {}, "counters": {}}
+    for pat, key in NAMES.items():
+        cs = acc.get(pat % K)
+        if not cs:
+            continue
+        mean = {c: sum(v) / len(v) for c, v in cs.items()}
+        rec["counters"][key] = mean
+        if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+            rec["hbm_bytes_per_launch"][key] = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1, sort_keys=True)
+    print(json.dumps(rec["hbm_bytes_per_launch"], indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
