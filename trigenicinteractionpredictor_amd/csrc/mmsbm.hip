@@ -275,7 +275,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ cbuf,
     double* __restrict__ prows, double* __restrict__ spart, double* __restrict__ pold,
     double* __restrict__ partL, int P, int R, long long n_rows0, long long n_prows, int n_wg,
-    int n_sp, double eps) {
+    int n_sp, double eps, int gcap) {
   using T = KT<K>;
   constexpr int NG = T::NG, TR = T::TR, VR = T::VR;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -308,8 +308,10 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   const int s = code >> 4, r = code & 15;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * T::K3;
   double* Vt = smem;
-  double* Tg = smem + (MODE == PASS_B ? 0 : T::GMAX * T::VDBL);  // theta rows of the V genes
-  double* img = smem + (MODE == PASS_B ? 0 : T::GMAX * (T::VDBL + T::KP)) + wv * T::IMGW;
+  // LDS: [gcap V tables][gcap theta rows][per-wave images]; gcap (<= GMAX) = the plan's most
+  // genes per stream-0 workgroup
+  double* Tg = smem + (MODE == PASS_B ? 0 : gcap * T::VDBL);  // theta rows of the V genes
+  double* img = smem + (MODE == PASS_B ? 0 : gcap * (T::VDBL + T::KP)) + wv * T::IMGW;
 
   // this wave's unit, and the first records of its pipeline (in flight during the V prologue).
   // Record stream: lane l < 16 holds int l of the chunk's 4 records (i, j, k, w), lane 16 the
@@ -340,15 +342,15 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     // vgenes holds GMAX (padded) genes per workgroup, so the theta loads do not wait for
     // wg_gene; p_r is staged in the image region when it fits.  All loads go out together.
     const int ng = wg_gene[w + 1] - wg_gene[w];
-    const int* __restrict__ vgw = vgenes + (size_t)w * T::GMAX;
+    const int* __restrict__ vgw = vgenes + (size_t)w * gcap;
     constexpr bool PV = T::K3 <= NW * T::IMGW;
-    double* Ps = smem + T::GMAX * (T::VDBL + T::KP);
+    double* Ps = smem + gcap * (T::VDBL + T::KP);
     constexpr int NTG = (T::GMAX * T::KP + NT - 1) / NT, NPV = PV ? (T::K3 + NT - 1) / NT : 1;
     double tg[NTG], pv[NPV];
 #pragma unroll
     for (int i = 0; i < NTG; ++i) {
       const int idx = tid + NT * i, gl = idx / T::KP, a = idx % T::KP;
-      const int g = vgw[gl < T::GMAX ? gl : 0];
+      const int g = vgw[gl < gcap ? gl : 0];
       tg[i] = th[(size_t)g * K + (a < K ? a : 0)];
     }
     if constexpr (PV) {
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 #pragma unroll
     for (int i = 0; i < NTG; ++i) {  // theta rows, zero padded
       const int idx = tid + NT * i, gl = idx / T::KP, a = idx % T::KP;
-      if (idx < T::GMAX * T::KP) Tg[idx] = (gl < ng && a < K) ? tg[i] : 0.0;
+      if (idx < gcap * T::KP) Tg[idx] = (gl < ng && a < K) ? tg[i] : 0.0;
     }
     if constexpr (PV) {
 #pragma unroll
@@ -1071,6 +1073,7 @@ struct mmsbm_ctx {
   int device = 0;
   int K = 0, R = 0, B = 0, P = 0;
   double eps = 1e-10;
+  int gcap = 0;                  // most pivot genes per stream-0 workgroup (<= KT<K>::GMAX)
   SetDev sets[2];
   int* deg = nullptr;            // device, owned
   std::vector<int> deg_host;
@@ -1154,22 +1157,24 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
         sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.wg_units + (size_t)h.n_wg_a * (NW + 1),
         sd.wg_code + h.n_wg_a, sd.wg_gene, sd.vgenes, sd.sp_desc, sd.prow_gene, theta, pr, c->cbuf,
         c->prows, c->spart, c->pold, c->partL, c->P, c->R, h.n_rows0, h.n_prows, h.n_wg_b, h.n_sp,
-        c->eps);
+        c->eps, c->gcap);
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
     int rc;
+    // dynamic LDS for the context's gene cap (<= the compile-time GMAX the opt-in covers)
+    const int lds = c->gcap * (T::VDBL + T::KP) * 8 + T::IMG_BYTES + 64;
     if (mode == PASS_A) {
       if ((rc = lds_opt_in(c, 0, &pass_kernel<K, PASS_A>, T::LDS_A))) return rc;
-      pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, c->B), NT, T::LDS_A, s>>>(
+      pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
           sd.sp_desc, sd.prow_gene, theta, pr, c->cbuf, c->prows, c->spart, c->pold, c->partL, c->P,
-          c->R, h.n_rows0, h.n_prows, h.n_wg_a, h.n_sp, c->eps);
+          c->R, h.n_rows0, h.n_prows, h.n_wg_a, h.n_sp, c->eps, c->gcap);
     } else {
       if ((rc = lds_opt_in(c, 1, &pass_kernel<K, PASS_LL>, T::LDS_A))) return rc;
-      pass_kernel<K, PASS_LL><<<dim3(h.n_wg_a, c->B), NT, T::LDS_A, s>>>(
+      pass_kernel<K, PASS_LL><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
           sd.sp_desc, sd.prow_gene, theta, pr, c->cbuf, c->prows, c->spart, c->pold, c->partL, c->P,
-          c->R, h.n_rows0, h.n_prows, h.n_wg_a, h.n_sp, c->eps);
+          c->R, h.n_rows0, h.n_prows, h.n_wg_a, h.n_sp, c->eps, c->gcap);
     }
   }
   HIP_TRY(hipGetLastError());
@@ -1336,6 +1341,13 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
   c->B = B;
   c->P = P;
   c->eps = eps;
+  // genes per stream-0 workgroup: the LDS budget's GMAX; MMSBM_GCAP=n lowers it (measurement:
+  // smaller V tables let more workgroups share a CU)
+  c->gcap = gmax_for(K);
+  if (const char* g = getenv("MMSBM_GCAP")) {
+    const int v = atoi(g);
+    if (v >= 4 && v < c->gcap) c->gcap = v;
+  }
   return MMSBM_OK;
 }
 
@@ -1368,7 +1380,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
     }
   }
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
-                           gmax_for(c->K));
+                           c->gcap);
   const auto& h = sd.h;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;
@@ -1377,7 +1389,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   if ((rc = upload(&sd.wg_code, h.wg_code))) return rc;
   if ((rc = upload(&sd.wg_gene, h.wg_gene))) return rc;
   {  // pivot genes padded to GMAX per stream-0 workgroup (the pass prologue indexes w GMAX + slot)
-    const int gm = gmax_for(c->K);
+    const int gm = c->gcap;
     const size_t nw = h.wg_gene.empty() ? 0 : h.wg_gene.size() - 1;
     std::vector<int> vpad(std::max<size_t>(nw * gm, 1), 0);
     for (size_t w = 0; w < nw; ++w) {
