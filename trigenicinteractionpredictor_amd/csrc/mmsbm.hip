@@ -264,7 +264,7 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
 // B[blk][k = hi][n = lo], D[blk][m = hi][n = lo] (tools/micro/mfma_layout.hip).
 //   Z   (blocks = b tiles, k = h):  A = th_v[obs lo][4 hs + hi], B = V_g[b][4 hs + hi]  -> Z[obs hi][b]
 //   M   (blocks = (x, y) tiles, k = the chunk's 4 observations):
-//       A = c_o th_u[obs hi][x], B = th_v[obs hi][y]  -> M[x = 4 xs + hi][y = 4 ys + lo]
+//       A = th_u[obs hi][x], B = c_o th_v[obs hi][y]  -> M[x = 4 xs + hi][y = 4 ys + lo]
 // ------------------------------------------------------------------------------------------
 template <int K, int MODE>
 __global__ __launch_bounds__(NT) void pass_kernel(
@@ -514,14 +514,15 @@ __global__ __launch_bounds__(NT) void pass_kernel(
           // ---- M += c th_u (x) th_v over the chunk's 4 observations
           // step ts: x tile ts / NGB (the same in every block), y tile 4 (ts % NGB) + blk, so a
           // lane reads NG A values and NGB B values per chunk
+          // c_o scales the B side (NGB values per lane instead of NG)
           double au[NG], bvv[T::NGB];
 #pragma unroll
-          for (int xs = 0; xs < NG; ++xs) au[xs] = c * I[hi * TR + 4 * xs + lo];
+          for (int xs = 0; xs < NG; ++xs) au[xs] = I[hi * TR + 4 * xs + lo];
 #pragma unroll
           for (int j = 0; j < T::NGB; ++j) {
             const int ys = 4 * j + blk;
             const double v = I[(4 + hi) * TR + (ys < NG ? 4 * ys + lo : 0)];
-            bvv[j] = ys < NG ? v : 0.0;
+            bvv[j] = ys < NG ? c * v : 0.0;
           }
 #pragma unroll
           for (int ts = 0; ts < T::NTS; ++ts) macc[ts] = mfma4(au[ts / T::NGB], bvv[ts % T::NGB], macc[ts]);
@@ -707,35 +708,53 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
   for (int t = 0; t < F::GT; ++t) acc[t] = 0.0;
   constexpr int NE = NGW * F::K2P;
   constexpr int NEPT = (NE + NT - 1) / NT, RE = NEPT < 12 ? NEPT : 12;
-  for (int combo = 0; combo < NC; ++combo) {
-    __syncthreads();
-    st_.mark(4);
-    for (int i0 = tid; i0 < NE; i0 += RE * NT) {
-      int qa[RE], qb[RE], kk[RE];
-      double v1[RE], v2[RE];
+  // one round of RE entries per thread: each entry's first two partial rows loaded with the whole
+  // round in flight (addresses clamped, loads unconditional); the first round of the next combo
+  // is loaded before this combo's contraction, so its latency hides under the MFMAs.  Only the
+  // loaded values stay live; ranges are re-read from LDS when the round is stored.
+  double v1[RE], v2[RE];
+  auto entry = [&](int combo, int idx, int& qa, int& qb, int& kk) {
+    const int gl = idx / F::K2P, k = idx % F::K2P;
+    const bool ok = idx < NE && k < K2;
+    qa = ok ? pp[combo][gl] : 0;
+    qb = ok ? pp[combo][gl + 1] : 0;
+    kk = k < K2 ? k : 0;
+  };
+  auto load_round = [&](int combo, int i0) {
 #pragma unroll
-      for (int u = 0; u < RE; ++u) {
-        const int idx = i0 + u * NT;
-        const int gl = idx / F::K2P, k = idx % F::K2P;
-        const bool ok = idx < NE && k < K2;
-        qa[u] = ok ? pp[combo][gl] : 0;
-        qb[u] = ok ? pp[combo][gl + 1] : 0;
-        kk[u] = k < K2 ? k : 0;
-        v1[u] = pb[(size_t)(qa[u] < qb[u] ? qa[u] : 0) * K2 + kk[u]];
-        v2[u] = pb[(size_t)(qa[u] + 1 < qb[u] ? qa[u] + 1 : 0) * K2 + kk[u]];
-      }
-#pragma unroll
-      for (int u = 0; u < RE; ++u) {
-        const int idx = i0 + u * NT;
-        double m = qa[u] < qb[u] ? v1[u] : 0.0;
-        if (qa[u] + 1 < qb[u]) m += v2[u];
-        for (int q = qa[u] + 2; q < qb[u]; ++q) m += pb[(size_t)q * K2 + kk[u]];
-        if (idx < NE) Ms[idx] = m;
-      }
-      st_.mark(5);
+    for (int u = 0; u < RE; ++u) {
+      int qa, qb, kk;
+      entry(combo, i0 + u * NT, qa, qb, kk);
+      v1[u] = pb[(size_t)(qa < qb ? qa : 0) * K2 + kk];
+      v2[u] = pb[(size_t)(qa + 1 < qb ? qa + 1 : 0) * K2 + kk];
     }
+  };
+  auto store_round = [&](int combo, int i0) {
+#pragma unroll
+    for (int u = 0; u < RE; ++u) {
+      const int idx = i0 + u * NT;
+      int qa, qb, kk;
+      entry(combo, idx, qa, qb, kk);
+      double m = qa < qb ? v1[u] : 0.0;
+      if (qa + 1 < qb) m += v2[u];
+      for (int q = qa + 2; q < qb; ++q) m += pb[(size_t)q * K2 + kk];
+      if (idx < NE) Ms[idx] = m;
+    }
+  };
+  __syncthreads();  // pp
+  load_round(0, tid);
+  for (int combo = 0; combo < NC; ++combo) {
+    __syncthreads();  // the previous combo's contraction is done with Ms
+    st_.mark(4);
+    store_round(combo, tid);
+    for (int i0 = tid + RE * NT; i0 < NE; i0 += RE * NT) {
+      load_round(combo, i0);
+      store_round(combo, i0);
+    }
+    st_.mark(5);
     __syncthreads();
     st_.mark(1);
+    if (combo + 1 < NC) load_round(combo + 1, tid);
     const int s = combo / R, r = combo % R;
     const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
     const double* __restrict__ Mg = Ms + (size_t)lo * F::K2P;
@@ -1380,7 +1399,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
     }
   }
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
-                           c->gcap);
+                           c->gcap, c->K <= 12 ? 16 : 4 * c->K);
   const auto& h = sd.h;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;

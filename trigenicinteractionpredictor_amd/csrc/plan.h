@@ -85,9 +85,10 @@ inline void pack_units(const std::vector<int>& run_chunks, int lmax, int gcap, s
 
 // Builds the plan.  units_a / units_b: the number of units to aim for in stream 0 and in streams
 // 1 + 2 together (about 8 waves per CU); gcap: most distinct genes per stream-0 workgroup (its
-// V table lives in LDS).
+// V table lives in LDS); sp_rows: stream-0 partial rows per S-partial workgroup (each writes a
+// K^3 partial, so large K wants more rows per partial).
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
-                  int units_a, int units_b, int gcap) {
+                  int units_a, int units_b, int gcap, int sp_rows = 16) {
   Plan pl;
   pl.R = R;
   pl.P = P;
@@ -287,7 +288,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       const int q1 = pl.prow_ptr[(size_t)r * (P + 1) + P];
       pl.sp_lo[r] = pl.n_sp;
       const int n = q1 - q0;
-      const int parts = n <= 0 ? 0 : std::min(256, std::max(1, n / 16));
+      const int parts = n <= 0 ? 0 : std::min(256, std::max(1, n / std::max(sp_rows, 1)));
       for (int k = 0; k < parts; ++k) {
         pl.sp_desc.push_back(r);
         pl.sp_desc.push_back(q0 + (int)((long long)n * k / parts));
