@@ -1,0 +1,59 @@
+"""The engine's work plan (csrc/plan.h, built by mmsbm_set_links) checked on the CPU: a small
+C++ driver (tests/plan_check.cpp) builds plans for synthetic link tables and checks their
+invariants — every observation once per stream, one pivot gene per chunk, unit and gene caps,
+chunk coverage, V slots, partial-row numbering per (stream, rating, gene), S-partial tiling."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def plan_check(tmp_path_factory):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = str(tmp_path_factory.mktemp("plan") / "plan_check")
+    subprocess.run([gxx, "-O2", "-std=c++17", "-o", exe, os.path.join(HERE, "plan_check.cpp")],
+                   check=True)
+    return exe
+
+
+def _links(P, E, seed, R=2, hub=0.0, multi=0.05, both=0.03):
+    rng = np.random.default_rng(seed)
+    p = np.ones(P)
+    if hub:
+        p[: max(1, P // 50)] *= hub  # a few genes with very long pivot runs
+    p /= p.sum()
+    seen, rows = set(), []
+    while len(rows) < E:
+        t = tuple(sorted(rng.choice(P, 3, p=p).tolist(), key=str))
+        if t in seen:
+            continue
+        seen.add(t)
+        c = [0] * R
+        r = int(rng.integers(R))
+        c[r] = int(rng.integers(2, 5)) if rng.random() < multi else 1
+        if rng.random() < both:
+            c[1 - r] = 1
+        rows.append(list(t) + c)
+    return np.array(rows, dtype=np.int64)
+
+
+@pytest.mark.parametrize("P,E,units,gcap,sp_rows,hub", [
+    (40, 600, (1, 1), 33, 16, 0.0),        # one unit per stream: every run split at 64 chunks
+    (200, 3000, (3, 5), 4, 16, 0.0),       # tiny gene cap: gene-capped workgroups
+    (300, 5000, (1536, 3072), 33, 16, 30.0),   # hub genes, default unit counts
+    (120, 4000, (64, 64), 13, 120, 10.0),  # large-K shape: 13 genes, 120 rows per S partial
+    (30, 1500, (1536, 3072), 8, 40, 0.0),  # more units than chunks
+])
+def test_plan_invariants(plan_check, P, E, units, gcap, sp_rows, hub):
+    links = _links(P, E, seed=P + E, hub=hub)
+    head = "%d 2 %d %d %d %d %d\n" % (len(links), P, units[0], units[1], gcap, sp_rows)
+    body = "\n".join(" ".join(str(v) for v in row) for row in links)
+    res = subprocess.run([plan_check], input=head + body + "\n", capture_output=True, text=True)
+    assert res.returncode == 0 and res.stdout.startswith("ok"), res.stdout + res.stderr
