@@ -101,9 +101,7 @@ struct KT {
   // S partials: (a-tile, group of 4 cell tiles) items over the 8 waves
   static constexpr int NCT = (K2 + 3) / 4;
   static constexpr int NCG = (NCT + 3) / 4;
-  static constexpr int NSI_ALL = (NG * NCG + NW - 1) / NW;
-  static constexpr int NSI = NSI_ALL < 8 ? NSI_ALL : 8;           // accumulators per wave
-  static constexpr int NIG = (NG * NCG + NW * NSI - 1) / (NW * NSI);  // item groups (workgroups)
+  static constexpr int NIG = (NCG + NW - 1) / NW;  // S partial: one cell group per wave, NIG workgroups
   static_assert(LDS_A <= 160 * 1024, "pass A LDS over budget");
   static_assert(64 * KP * 8 <= IMG_BYTES, "S partial staging over the pass B LDS");
 };
@@ -187,7 +185,8 @@ enum { PASS_A = 0, PASS_LL = 1, PASS_B = 2 };
 // ------------------------------------------------------------------------------------------
 // S partial of one workgroup (launch B): S_r[a][cell] += th_g(q)[a] M_q[cell] over the partial rows
 // q of stream 0, rating r, in [q0, q1), cells (b, h) dense.  MFMA k index = four partial rows,
-// blocks = four cell tiles, wave wv owns the (a-tile, cell group) items wv, wv + 8, ...
+// blocks = four cell tiles; wave wv of item group ig owns cell group cg = ig NW + wv (16 cells)
+// for every a tile, so each partial-row value is loaded once and feeds NG MFMAs.
 // ------------------------------------------------------------------------------------------
 template <int K>
 __device__ __forceinline__ void s_partial(const double* __restrict__ th, const double* __restrict__ prows_b,
@@ -195,12 +194,18 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
                                           double* __restrict__ out, double* __restrict__ Tq, int ig,
                                           int tid, int wv, int hi, int blk, int lo, Stamp& st_) {
   using T = KT<K>;
+  constexpr int NG = T::NG;
   // blocks of QB partial rows: their genes' theta rows staged in LDS (zero padded), so the loop
-  // over the block only streams the partial rows themselves from HBM
-  constexpr int QB = 64, NI = (QB * T::KP + NT - 1) / NT;
-  double acc[T::NSI];
+  // over the block only streams the partial rows themselves
+  constexpr int QB = 64, NI = (QB * T::KP + NT - 1) / NT, RS = K <= 12 ? 4 : 8;  // steps per round
+  const int cg = ig * NW + wv;
+  const bool cgv = cg < T::NCG;
+  const int cell = 4 * (4 * (cgv ? cg : 0) + blk) + lo;
+  const bool cv = cgv && cell < T::K2;
+  const int cellc = cv ? cell : 0;
+  double acc[NG];
 #pragma unroll
-  for (int k = 0; k < T::NSI; ++k) acc[k] = 0.0;
+  for (int t = 0; t < NG; ++t) acc[t] = 0.0;
   for (int qb = q0; qb < q1; qb += QB) {
     const int nq = q1 - qb < QB ? q1 - qb : QB;
     __syncthreads();
@@ -217,41 +222,29 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
       if (tid + NT * i < QB * T::KP) Tq[tid + NT * i] = x[i];
     __syncthreads();
     st_.mark(1);
-    for (int qq = 0; qq < nq; qq += 16) {  // 4 MFMA steps per round, their loads issued together
-      double m[4][T::NSI];
+    for (int qq = 0; qq < nq; qq += 4 * RS) {  // RS steps of 4 rows per round, loads together
+      double m[RS];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool vq = qq + 4 * u + hi < nq;
-        const double* __restrict__ Mq = prows_b + (size_t)(qb + (vq ? qq + 4 * u + hi : 0)) * T::K2;
-#pragma unroll
-        for (int k = 0; k < T::NSI; ++k) {
-          const int it = ig * NW * T::NSI + wv + NW * k;
-          const int cg = it % T::NCG, cell = 4 * (4 * cg + blk) + lo;
-          const double v = Mq[cell < T::K2 ? cell : 0];
-          m[u][k] = (vq && cell < T::K2) ? v : 0.0;
-        }
+      for (int u = 0; u < RS; ++u) {
+        const int row = qq + 4 * u + hi;
+        const bool vq = row < nq;
+        const double v = prows_b[(size_t)(qb + (vq ? row : 0)) * T::K2 + cellc];
+        m[u] = (vq && cv) ? v : 0.0;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RS; ++u) {
+        const int row = qq + 4 * u + hi;  // Tq rows past nq (and past QB) read as zero
+        const double* tq = Tq + (row < QB ? row : 0) * T::KP;
 #pragma unroll
-        for (int k = 0; k < T::NSI; ++k) {
-          const int it = ig * NW * T::NSI + wv + NW * k;
-          if (it < T::NG * T::NCG) {
-            const int a = 4 * (it / T::NCG) + lo;
-            // zero for a >= K and for rows past nq (Tq holds QB rows)
-            acc[k] = mfma4(Tq[(qq + 4 * u + hi) * T::KP + a], m[u][k], acc[k]);
-          }
-        }
+        for (int t = 0; t < NG; ++t) acc[t] = mfma4(row < QB ? tq[4 * t + lo] : 0.0, m[u], acc[t]);
       }
     }
   }
+  if (cgv) {
 #pragma unroll
-  for (int k = 0; k < T::NSI; ++k) {
-    const int it = ig * NW * T::NSI + wv + NW * k;
-    if (it < T::NG * T::NCG) {
-      const int at = it / T::NCG, cg = it % T::NCG;
-      const int a = 4 * at + hi, cell = 4 * (4 * cg + blk) + lo;
-      if (a < K && cell < T::K2) st_wt(out + (size_t)a * T::K2 + cell, acc[k]);
+    for (int t = 0; t < NG; ++t) {
+      const int a = 4 * t + hi;
+      if (a < K && cell < T::K2) st_wt(out + (size_t)a * T::K2 + cell, acc[t]);
     }
   }
   st_.mark(2);
