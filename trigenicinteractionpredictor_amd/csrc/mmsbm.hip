@@ -370,36 +370,41 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     constexpr int CT = K * NG;  // (b, h tile) cell tiles
     constexpr int CG = (CT + 3) / 4;
     const int GT = (ng + 3) / 4;
-    // items (gene tile, 4 cell tiles); IPR per round: independent MFMA chains, reads together
-    constexpr int IPR = 2;
-    for (int i0 = wv; i0 < GT * CG; i0 += IPR * NW) {
-      double av[IPR][NG], bv[IPR][NG];
+    constexpr int GTM = (T::GMAX + 3) / 4;
+    // wave wv owns cell groups (4 cell tiles) cg = wv, wv + NW, ..., CPR per round, for every
+    // gene tile: each p value is loaded once and feeds GT MFMAs (A = the tile's theta rows)
+    constexpr int CPR = K <= 12 ? 1 : 2;
+    for (int c0 = wv; c0 < CG; c0 += CPR * NW) {
+      double bv[CPR][NG];
+      int ctv[CPR];
 #pragma unroll
-      for (int u = 0; u < IPR; ++u) {
-        const int item = i0 + u * NW;
-        const bool iv = item < GT * CG;
-        const int gt = iv ? item / CG : 0, cg = iv ? item % CG : 0;
-        const int ct = 4 * cg + blk;
-        const bool cv = iv && ct < CT;
+      for (int u = 0; u < CPR; ++u) {
+        const int ct = 4 * (c0 + u * NW) + blk;
+        const bool cv = c0 + u * NW < CG && ct < CT;
         const int bb = cv ? ct / NG : 0, hh = cv ? 4 * (ct % NG) + lo : 0;
+        ctv[u] = cv ? ct : -1;
 #pragma unroll
         for (int as = 0; as < NG; ++as) {
           const int a = 4 * as + hi;
-          av[u][as] = Tg[(4 * gt + lo) * T::KP + a];
           bv[u][as] = (cv && a < K && hh < K) ? pv_src[(a * K + bb) * K + hh] : 0.0;
         }
       }
 #pragma unroll
-      for (int u = 0; u < IPR; ++u) {
-        const int item = i0 + u * NW;
-        double acc = 0.0;
+      for (int u = 0; u < CPR; ++u) {
+        double acc[GTM];
 #pragma unroll
-        for (int as = 0; as < NG; ++as) acc = mfma4(av[u][as], bv[u][as], acc);
-        const int gt = item / CG, cg = item % CG;
-        const int ct = 4 * cg + blk;
-        const int go = 4 * gt + hi;
-        if (item < GT * CG && ct < CT && go < ng)
-          Vt[go * T::VDBL + (ct / NG) * VR + 4 * (ct % NG) + lo] = acc;
+        for (int t = 0; t < GTM; ++t) acc[t] = 0.0;
+#pragma unroll
+        for (int as = 0; as < NG; ++as)
+#pragma unroll
+          for (int t = 0; t < GTM; ++t)
+            if (t < GT) acc[t] = mfma4(Tg[(4 * t + lo) * T::KP + 4 * as + hi], bv[u][as], acc[t]);
+        const int ct = ctv[u];
+#pragma unroll
+        for (int t = 0; t < GTM; ++t) {
+          const int go = 4 * t + hi;
+          if (t < GT && ct >= 0 && go < ng) Vt[go * T::VDBL + (ct / NG) * VR + 4 * (ct % NG) + lo] = acc[t];
+        }
       }
     }
     __syncthreads();
