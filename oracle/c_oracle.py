@@ -39,14 +39,25 @@ def lib():
         L.oracle_predict.restype = None
         L.oracle_predict.argtypes = [ctypes.c_int64, P_i32, ctypes.c_int, ctypes.c_int,
                                      P_f64, P_f64, P_f64]
+        L.oracle_pair_loglik.restype = ctypes.c_double
+        L.oracle_pair_loglik.argtypes = [ctypes.c_int64, P_i32, P_i32, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_double, P_f64, P_f64]
+        L.oracle_joint_make_iteration.restype = ctypes.c_int
+        L.oracle_joint_make_iteration.argtypes = [ctypes.c_int64, P_i32, P_i32, ctypes.c_int64, P_i32,
+                                                  P_i32, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_double, P_f64, P_f64, P_f64]
+        L.oracle_pair_predict.restype = None
+        L.oracle_pair_predict.argtypes = [ctypes.c_int64, P_i32, ctypes.c_int, ctypes.c_int,
+                                          P_f64, P_f64, P_f64]
         _lib = L
     return _lib
 
 
-def links_to_arrays(links: dict, R: int = 2):
-    """`links` dict ("i_j_k" -> [n0, n1]) in insertion order -> (ids, counts)."""
+def links_to_arrays(links: dict, R: int = 2, arity: int = 3):
+    """`links` dict ("i_j_k" -> [n0, n1]; "i_j" for `dlinks`, arity 2) in insertion order
+    -> (ids, counts)."""
     E = len(links)
-    ids = np.empty((E, 3), dtype=np.int32)
+    ids = np.empty((E, arity), dtype=np.int32)
     counts = np.empty((E, R), dtype=np.int32)
     for e, (key, n) in enumerate(links.items()):
         ids[e] = [int(s) for s in key.split("_")]
@@ -78,4 +89,46 @@ def predict(ids, theta, pr):
     out = np.empty(ids.shape[0], dtype=np.float64)
     lib().oracle_predict(ids.shape[0], np.ascontiguousarray(ids), K, pr.shape[-1],
                          np.ascontiguousarray(theta), np.ascontiguousarray(pr), out)
+    return out
+
+
+# ---- joint digenic + trigenic model (src/TrigenicInteractionPredictor_23.py) ----
+# ids2 int32[E2][2], counts2 int32[E2][R], qr f64[K][K][R].
+
+def pair_loglik(ids2, counts2, theta, qr, eps=1e-10):
+    K = theta.shape[1]
+    R = counts2.shape[1]
+    return lib().oracle_pair_loglik(ids2.shape[0], np.ascontiguousarray(ids2, dtype=np.int32),
+                                    np.ascontiguousarray(counts2, dtype=np.int32), K, R, eps,
+                                    np.ascontiguousarray(theta), np.ascontiguousarray(qr))
+
+
+def joint_loglik(ids3, counts3, ids2, counts2, theta, pr, qr, eps=1e-10):
+    """compute_likelihood of the joint model (:1534-1562): triplets then pairs."""
+    return loglik(ids3, counts3, theta, pr, eps) + pair_loglik(ids2, counts2, theta, qr, eps)
+
+
+def joint_make_iteration(ids3, counts3, ids2, counts2, theta, pr, qr, eps=1e-10):
+    """Returns new (theta, pr, qr) of :1572-1687; raises ZeroDivisionError like :1642."""
+    theta = np.array(theta, dtype=np.float64, copy=True, order="C")
+    pr = np.array(pr, dtype=np.float64, copy=True, order="C")
+    qr = np.array(qr, dtype=np.float64, copy=True, order="C")
+    P, K = theta.shape
+    R = qr.shape[-1]
+    ids3 = np.ascontiguousarray(ids3, dtype=np.int32).reshape(-1, 3)
+    counts3 = np.ascontiguousarray(counts3, dtype=np.int32).reshape(-1, R)
+    ids2 = np.ascontiguousarray(ids2, dtype=np.int32).reshape(-1, 2)
+    counts2 = np.ascontiguousarray(counts2, dtype=np.int32).reshape(-1, R)
+    rc = lib().oracle_joint_make_iteration(ids3.shape[0], ids3, counts3, ids2.shape[0], ids2, counts2,
+                                           P, K, R, eps, theta, pr, qr)
+    if rc != 0:
+        raise ZeroDivisionError("float division by zero")
+    return theta, pr, qr
+
+
+def pair_predict(ids2, theta, qr):
+    K = theta.shape[1]
+    out = np.empty(ids2.shape[0], dtype=np.float64)
+    lib().oracle_pair_predict(ids2.shape[0], np.ascontiguousarray(ids2, dtype=np.int32), K, qr.shape[-1],
+                              np.ascontiguousarray(theta), np.ascontiguousarray(qr), out)
     return out

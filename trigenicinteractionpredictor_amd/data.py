@@ -20,7 +20,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-__all__ = ["FoldSpec", "FOLD0", "write_fold", "gene_name"]
+__all__ = ["FoldSpec", "FOLD0", "write_fold", "gene_name", "JointFoldSpec", "write_joint_fold"]
 
 
 def gene_name(idx: int) -> str:
@@ -178,3 +178,82 @@ def synthetic_links(spec: FoldSpec):
     counts = np.zeros((train.shape[0], 2), dtype=np.int32)
     counts[np.arange(train.shape[0]), r] = 1
     return np.ascontiguousarray(train), counts
+
+
+# ---- joint digenic + trigenic folds (src/TrigenicInteractionPredictor_23.py) ----
+HO_DELTA = "hoΔ"   # filler allele the joint reader drops from every key (:405-410)
+
+
+@dataclass(frozen=True)
+class JointFoldSpec:
+    """A fold with triplet lines ``a_b_c\\t<r>`` and pair lines ``a_b\\t<r>`` mixed in one
+    file, as `get_train_test` (:393-546) reads them.  Triplets use genes ``[0, P - pair_only)``;
+    the last ``pair_only`` genes appear only in pairs, so their degree comes from the pair loop
+    alone (:1616-1617).  ``ho_frac`` of the pair lines carry the filler allele as a third name."""
+
+    P: int
+    E3: int
+    E2: int
+    seed: int = 7
+    pos_frac: float = 0.05
+    pair_pos_frac: float = 0.1
+    test_frac: float = 0.2
+    multi_frac: float = 0.0
+    both_frac: float = 0.0
+    pair_only: int = 0
+    ho_frac: float = 0.0
+
+
+def write_joint_fold(spec: JointFoldSpec, train_path: str, test_path: str) -> tuple[int, int]:
+    """Write a synthetic joint train/test fold; returns (#train lines, #test lines)."""
+    rng = random.Random(spec.seed)
+    P3 = spec.P - spec.pair_only
+    if spec.E3:
+        cover, rest = _python_triples(FoldSpec(P=P3, E=spec.E3, seed=spec.seed), rng)
+    else:
+        cover, rest = [], []
+    pairs, seen = [], set()
+    only = list(range(P3, spec.P))
+    for s in range(0, len(only)):   # cover: each pair-only gene with a random partner
+        b = rng.randrange(spec.P - 1)
+        b = b if b < only[s] else b + 1
+        key = tuple(sorted((only[s], b)))
+        if key not in seen:
+            seen.add(key)
+            pairs.append(key)
+    while len(pairs) < spec.E2:
+        key = tuple(sorted(rng.sample(range(spec.P), 2)))
+        if key not in seen:
+            seen.add(key)
+            pairs.append(key)
+    ncover = len(only)
+    n3_test = min(int(spec.E3 * spec.test_frac), len(rest))
+    n2_test = min(int(spec.E2 * spec.test_frac), len(pairs) - ncover)
+    test_keys = rest[:n3_test] + pairs[len(pairs) - n2_test:]
+    train_keys = cover + rest[n3_test:] + pairs[:len(pairs) - n2_test]
+    rating = {}
+    for key in train_keys + test_keys:
+        frac = spec.pos_frac if len(key) == 3 else spec.pair_pos_frac
+        rating[key] = 1 if rng.random() < frac else 0
+
+    def names(key):
+        n = [gene_name(g) for g in key]
+        if len(key) == 2 and spec.ho_frac and rng.random() < spec.ho_frac:
+            n.append(HO_DELTA)
+        return sorted(n)
+
+    train_lines = [_line(names(k), rating[k]) for k in train_keys]
+    for k in train_keys:
+        if spec.multi_frac and rng.random() < spec.multi_frac:
+            train_lines += [_line(names(k), rating[k])] * rng.randint(1, 3)
+        if spec.both_frac and rng.random() < spec.both_frac:
+            train_lines.append(_line(names(k), 1 - rating[k]))
+    test_lines = [_line(names(k), rating[k]) for k in test_keys]
+    rng.shuffle(train_lines)
+    rng.shuffle(test_lines)
+    for path, lines in ((train_path, train_lines), (test_path, test_lines)):
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        with open(path, "w", encoding="utf-8") as f:
+            f.writelines(lines)
+    return len(train_lines), len(test_lines)
