@@ -41,7 +41,7 @@ def lib():
                                      P_f64, P_f64, P_f64]
         L.oracle_pair_loglik.restype = ctypes.c_double
         L.oracle_pair_loglik.argtypes = [ctypes.c_int64, P_i32, P_i32, ctypes.c_int, ctypes.c_int,
-                                         ctypes.c_double, P_f64, P_f64]
+                                         ctypes.c_double, P_f64, P_f64, ctypes.c_double]
         L.oracle_joint_make_iteration.restype = ctypes.c_int
         L.oracle_joint_make_iteration.argtypes = [ctypes.c_int64, P_i32, P_i32, ctypes.c_int64, P_i32,
                                                   P_i32, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -95,17 +95,17 @@ def predict(ids, theta, pr):
 # ---- joint digenic + trigenic model (src/TrigenicInteractionPredictor_23.py) ----
 # ids2 int32[E2][2], counts2 int32[E2][R], qr f64[K][K][R].
 
-def pair_loglik(ids2, counts2, theta, qr, eps=1e-10):
+def pair_loglik(ids2, counts2, theta, qr, eps=1e-10, start=0.0):
     K = theta.shape[1]
     R = counts2.shape[1]
     return lib().oracle_pair_loglik(ids2.shape[0], np.ascontiguousarray(ids2, dtype=np.int32),
                                     np.ascontiguousarray(counts2, dtype=np.int32), K, R, eps,
-                                    np.ascontiguousarray(theta), np.ascontiguousarray(qr))
+                                    np.ascontiguousarray(theta), np.ascontiguousarray(qr), start)
 
 
 def joint_loglik(ids3, counts3, ids2, counts2, theta, pr, qr, eps=1e-10):
-    """compute_likelihood of the joint model (:1534-1562): triplets then pairs."""
-    return loglik(ids3, counts3, theta, pr, eps) + pair_loglik(ids2, counts2, theta, qr, eps)
+    """compute_likelihood of the joint model (:1534-1562): one running sum, triplets then pairs."""
+    return pair_loglik(ids2, counts2, theta, qr, eps, start=loglik(ids3, counts3, theta, pr, eps))
 
 
 def joint_make_iteration(ids3, counts3, ids2, counts2, theta, pr, qr, eps=1e-10):

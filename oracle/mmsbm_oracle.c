@@ -115,11 +115,13 @@ int oracle_make_iteration(int64_t E, const int32_t *ids, const int32_t *counts,
  * pair links: ids2 int32[E2][2] (`dlinks` keys, string-sorted ids), counts2 int32[E2][R],
  * qr f64[K][K][R] (:163-174). */
 
-/* compute_likelihood's pair loop, :1549-1559 */
+/* compute_likelihood's pair loop, :1549-1559, continuing the running sum `start` of the
+ * triplet loop (:1535-1547) */
 double oracle_pair_loglik(int64_t E, const int32_t *ids, const int32_t *counts,
-                          int K, int R, double eps, const double *theta, const double *qr)
+                          int K, int R, double eps, const double *theta, const double *qr,
+                          double start)
 {
-    double total = 0.0;
+    double total = start;
     double d[16];
     for (int64_t e = 0; e < E; ++e) {
         const double *t1 = theta + (int64_t)ids[2 * e + 0] * K;

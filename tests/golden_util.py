@@ -73,3 +73,22 @@ def compare_output(got, want, rtol=1e-9, gap=1e-7):
         if lo and hi:
             assert rows_g[i][1:] == rows_w[i][1:], (i, rows_g[i], rows_w[i])
     assert sorted(tuple(r[1:]) for r in rows_g) == sorted(tuple(r[1:]) for r in rows_w)
+
+
+# ---- joint digenic + trigenic fixtures (tests/golden/make_joint_golden.py) ----
+JOINT = os.path.join(GOLDEN, "joint")
+
+
+def joint_cases():
+    out = []
+    for meta_path in sorted(glob.glob(os.path.join(JOINT, "*", "K*_s*.json"))):
+        out.append((os.path.basename(os.path.dirname(meta_path)), os.path.basename(meta_path)[:-5]))
+    return out
+
+
+def joint_load(case, name):
+    d = os.path.join(JOINT, case)
+    with open(os.path.join(d, name + ".json"), encoding="utf-8") as f:
+        meta = json.load(f)
+    vec = np.load(os.path.join(d, name + ".npz"), allow_pickle=False)
+    return meta, vec, os.path.join(d, "train.dat"), os.path.join(d, "test.dat")
