@@ -1,0 +1,87 @@
+/*
+ * mmsbm_pairs.h — C ABI of the pair lattice of the joint digenic + trigenic model
+ * (libmmsbm.so, the same library as mmsbm.h).
+ *
+ * Reference: AleixMT/TrigenicInteractionPredictor, src/TrigenicInteractionPredictor_23.py,
+ * under the spec fix in DESIGN.md (DataType.ALL, which :105 names, reads as DataType.all).
+ * The joint model keeps the triplet lattice pr of mmsbm.h and adds, for digenic links
+ * (`dlinks`, :364-374), a K x K lattice qr sharing theta (:163-174):
+ *
+ *   dd = eps + sum_ab th_i[a] th_j[b] q_r[a][b],   c = n / dd                 (:1623-1626)
+ *   ntheta[i][a] += c th_i[a] (q_r th_j)[a],  ntheta[j][b] += c th_j[b] (q_r^T th_i)[b]
+ *   nqr[a][b][r] += c th_i[a] th_j[b] q_r[a][b]                               (:1628-1635)
+ *
+ * into the SAME ntheta and counter as the triplet loop (:1575-1607); then
+ * theta = ntheta / counter (:1639-1642), pr and qr normalised over r (:1652-1666).
+ *
+ * One joint iteration through the two ABIs (what trigenicinteractionpredictor_amd/joint.py
+ * runs; tri = an mmsbm_ctx holding `links` and, via mmsbm_set_degree, the JOINT counter):
+ *   mmsbm_accumulate(tri, theta, pr, nth, S)          triplet sums (theta not applied)
+ *   mmsbm_pairs_accumulate(pc, theta, qr, nth, S2)    adds the pair sums into nth, writes S2
+ *   mmsbm_mstep(tri, theta, pr, nth, S)               theta <- theta nth / counter, pr
+ *   mmsbm_pairs_qstep(pc, qr, S2)                     qr <- qr S2 / (eps + sum_r qr S2)
+ *
+ * Conventions are those of mmsbm.h (return codes, mmsbm_last_error, _host = host arrays,
+ * everything else device, kernels on the caller's stream, one host thread per context).
+ *
+ * Device layouts
+ *  - theta f64[B][P][K]          (shared with the triplet lattice)
+ *  - qr    f64[B][R][K][K]       rating-major copy of the reference's qr[K][K][R]
+ *  - nth   f64[B][P][K]          in/out of mmsbm_pairs_accumulate (pair sums ADDED)
+ *  - S2    f64[B][R][K][K]       pair lattice sums, nqr = qr S2
+ */
+#ifndef MMSBM_PAIRS_H
+#define MMSBM_PAIRS_H
+
+#include <stdint.h>
+
+#include "mmsbm.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mmsbm_pairs_ctx mmsbm_pairs_ctx;
+
+/* Context = one GPU + one shape; replaces the pair half of the `_23` Model state (:43-105). */
+int mmsbm_pairs_create(int device, mmsbm_pairs_ctx **out);
+int mmsbm_pairs_destroy(mmsbm_pairs_ctx *ctx);
+int mmsbm_pairs_set_shape(mmsbm_pairs_ctx *ctx, int32_t K, int32_t R, int32_t B, int32_t P, double eps);
+
+/* One pair-link set (MMSBM_SET_TRAIN = `dlinks`, MMSBM_SET_TEST = `dtest_links`) as
+ * get_train_test (:393-546) leaves it, in dict order: ids_host[E][2] = the key's ids in its
+ * string-sorted order, counts_host[E][R] = dlinks[key].  Builds the device plan
+ * (observations and, for the train set, the per-gene gather lists).  Invalidates the
+ * workspace. */
+int mmsbm_pairs_set_links(mmsbm_pairs_ctx *ctx, int32_t which, const int32_t *ids_host,
+                          const int32_t *counts_host, int64_t E);
+int mmsbm_pairs_workspace_bytes(const mmsbm_pairs_ctx *ctx, int64_t *bytes);
+int mmsbm_pairs_set_workspace(mmsbm_pairs_ctx *ctx, void *ws, int64_t bytes);
+
+/* The pair loop of make_iteration (:1608-1635): nth[B][P][K] += the pair sums (theta not
+ * applied), S2[B][R][K^2] = the pair lattice sums.  With no train pairs nth is untouched and
+ * S2 is zeroed. */
+int mmsbm_pairs_accumulate(mmsbm_pairs_ctx *ctx, const double *theta, const double *qr, double *nth,
+                           double *S2, void *stream);
+
+/* qr <- qr S2 / (eps + sum_r qr S2) (:1660-1666, :1674-1676). */
+int mmsbm_pairs_qstep(mmsbm_pairs_ctx *ctx, double *qr, const double *S2, void *stream);
+
+/* The pair loop of compute_likelihood (:1549-1559): out[B] = sum over pair links of
+ * sum_r n_r log dd_r for set `which`. */
+int mmsbm_pairs_loglik(mmsbm_pairs_ctx *ctx, int32_t which, const double *theta, const double *qr,
+                       double *out, void *stream);
+
+/* do_prediction of a pair (:957-962): P(r = 1) = sum_ab th_i[a] th_j[b] q_1[a][b] for n rows
+ * of ids int32[n][2] into out[B][n]; an id outside [0, P) gives NaN. */
+int mmsbm_pairs_predict(mmsbm_pairs_ctx *ctx, const int32_t *ids, int64_t n, const double *theta,
+                        const double *qr, double *out, void *stream);
+
+/* Measurement: info[4] = observations (train), gather entries, gather workgroups,
+ * likelihood workgroups of set `which`. */
+int mmsbm_pairs_plan_info(const mmsbm_pairs_ctx *ctx, int32_t which, int64_t *info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMSBM_PAIRS_H */

@@ -1,4 +1,5 @@
-"""The C-ABI library builds, loads and exports every symbol include/mmsbm.h declares.
+"""The C-ABI library builds, loads and exports every symbol include/mmsbm.h and
+include/mmsbm_pairs.h declare.
 No compute calls: this runs on the CPU-only build container."""
 import ctypes
 import os
@@ -7,11 +8,11 @@ import re
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(REPO, "include", "mmsbm.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("mmsbm.h", "mmsbm_pairs.h")]
 
 
 def declared_symbols():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(mmsbm_\w+)\s*\(", text, re.M)))
 
 
@@ -24,7 +25,8 @@ def lib():
 
 def test_header_declares_the_abi():
     syms = declared_symbols()
-    for need in ("mmsbm_create", "mmsbm_set_links", "mmsbm_iterate", "mmsbm_loglik", "mmsbm_predict"):
+    for need in ("mmsbm_create", "mmsbm_set_links", "mmsbm_iterate", "mmsbm_loglik", "mmsbm_predict",
+                 "mmsbm_pairs_accumulate", "mmsbm_pairs_qstep", "mmsbm_pairs_loglik"):
         assert need in syms
 
 
@@ -46,6 +48,10 @@ def test_constants_and_error_string(lib):
     assert lib.mmsbm_create(0, None) == _lib.MMSBM_ERR_INVALID
     assert b"null" in lib.mmsbm_last_error()
     assert lib.mmsbm_set_shape(None, 10, 2, 1, 10, 1e-10) == _lib.MMSBM_ERR_INVALID
+    # the pair ABI reports through the same error channel
+    assert lib.mmsbm_pairs_create(0, None) == _lib.MMSBM_ERR_INVALID
+    assert b"null" in lib.mmsbm_last_error()
+    assert lib.mmsbm_pairs_set_shape(None, 10, 2, 1, 10, 1e-10) == _lib.MMSBM_ERR_INVALID
 
 
 def test_library_is_gfx950_code_object():

@@ -47,6 +47,18 @@ SIGNATURES = {
     "mmsbm_timing": (_c_int, [_vp, _c_i32]),
     "mmsbm_timing_result": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_i64)]),
     "mmsbm_time_kernel": (_c_int, [_vp, _c_i32, _vp, _vp, _c_i32, _vp, ctypes.POINTER(_c_dbl)]),
+    # include/mmsbm_pairs.h — the joint model's pair lattice
+    "mmsbm_pairs_create": (_c_int, [_c_int, ctypes.POINTER(_vp)]),
+    "mmsbm_pairs_destroy": (_c_int, [_vp]),
+    "mmsbm_pairs_set_shape": (_c_int, [_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_dbl]),
+    "mmsbm_pairs_set_links": (_c_int, [_vp, _c_i32, _vp, _vp, _c_i64]),
+    "mmsbm_pairs_workspace_bytes": (_c_int, [_vp, ctypes.POINTER(_c_i64)]),
+    "mmsbm_pairs_set_workspace": (_c_int, [_vp, _vp, _c_i64]),
+    "mmsbm_pairs_accumulate": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmsbm_pairs_qstep": (_c_int, [_vp, _vp, _vp, _vp]),
+    "mmsbm_pairs_loglik": (_c_int, [_vp, _c_i32, _vp, _vp, _vp, _vp]),
+    "mmsbm_pairs_predict": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _vp, _vp]),
+    "mmsbm_pairs_plan_info": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i64)]),
 }
 
 _lib = None

@@ -12,13 +12,19 @@ import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
-SRC = os.path.join(PKG, "csrc", "mmsbm.hip")
+SRC = os.path.join(PKG, "csrc", "mmsbm.hip")           # triplet engine (include/mmsbm.h)
+SRC_PAIRS = os.path.join(PKG, "csrc", "pairs.hip")     # joint model pair lattice (mmsbm_pairs.h)
+SRCS = [SRC, SRC_PAIRS]
 INCLUDE = os.path.join(REPO, "include")
 OUT_DIR = os.path.join(PKG, "_build")
 LIB = os.path.join(OUT_DIR, "libmmsbm.so")
 SRC_IO = os.path.join(PKG, "csrc", "fold_io.cpp")
 LIB_IO = os.path.join(OUT_DIR, "libmmsbm_io.so")  # host-only ingestion (include/mmsbm_io.h)
 ARCH = os.environ.get("MMSBM_OFFLOAD_ARCH", "gfx950")
+DEPS = {
+    SRC: [os.path.join(PKG, "csrc", "plan.h"), os.path.join(INCLUDE, "mmsbm.h")],
+    SRC_PAIRS: [os.path.join(INCLUDE, "mmsbm.h"), os.path.join(INCLUDE, "mmsbm_pairs.h")],
+}
 
 
 def hipcc() -> str:
@@ -28,25 +34,57 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the MMSBM engine needs ROCm's hipcc to build")
 
 
+def _obj(src: str, out_dir: str = OUT_DIR, tag: str = "") -> str:
+    return os.path.join(out_dir, os.path.basename(src).replace(".hip", tag + ".o"))
+
+
+def compile_command(src: str, obj: str, extra=()) -> list[str]:
+    return [hipcc(), "-O3", "-std=c++17", "--offload-arch=" + ARCH, "-fPIC", "-c",
+            "-I" + INCLUDE, "-o", obj, src, *extra]
+
+
+def link_command(out: str, objs) -> list[str]:
+    return [hipcc(), "--offload-arch=" + ARCH, "-fPIC", "-shared", "-o", out, *objs]
+
+
 def command(out: str = LIB, extra=()) -> list[str]:
+    """One-shot build of every source into `out` (measurement builds with extra -D flags)."""
     return [hipcc(), "-O3", "-std=c++17", "--offload-arch=" + ARCH, "-fPIC", "-shared",
-            "-I" + INCLUDE, "-o", out, SRC, *extra]
+            "-I" + INCLUDE, "-o", out, *SRCS, *extra]
 
 
-def needs_build(out: str = LIB) -> bool:
-    if not os.path.exists(out):
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
         return True
-    t = os.path.getmtime(out)
-    deps = [SRC, os.path.join(PKG, "csrc", "plan.h"), os.path.join(INCLUDE, "mmsbm.h")]
+    t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def needs_build(out: str = LIB) -> bool:
+    return _stale(out, [d for src in SRCS for d in [src, *DEPS[src]]])
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
+    """Compile each source to an object (in parallel, only the stale ones) and link."""
     if not force and not needs_build():
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
+    procs = []
+    objs = []
+    for src in SRCS:
+        obj = _obj(src)
+        objs.append(obj)
+        if force or _stale(obj, [src, *DEPS[src]]):
+            cmd = compile_command(src, obj + ".tmp")
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            procs.append((subprocess.Popen(cmd), obj))
+    for p, obj in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, "hipcc " + obj)
+        os.replace(obj + ".tmp", obj)
     tmp = LIB + ".tmp"
-    cmd = command(tmp)
+    cmd = link_command(tmp, objs)
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

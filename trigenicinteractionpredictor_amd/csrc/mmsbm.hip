@@ -1308,6 +1308,13 @@ int set_degree(mmsbm_ctx* c, const std::vector<int>& deg) {
 
 }  // namespace
 
+// One error channel for the whole library: pairs.hip (the joint model's pair lattice, same .so)
+// reports through mmsbm_last_error too.
+int mmsbm_detail_fail(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+
 extern "C" {
 
 int mmsbm_version(void) { return 2; }
