@@ -110,6 +110,12 @@ int mmsbm_accumulate(mmsbm_ctx *ctx, const double *theta, const double *pr, doub
 int mmsbm_mstep(mmsbm_ctx *ctx, double *theta, double *pr, const double *nth, const double *S,
                 void *stream);
 
+/* Joint digenic + trigenic model (include/mmsbm_pairs.h): nth_add[B][P][K] (device; NULL = none)
+ * is added to every gene's triplet sums before the division by the counter in mmsbm_iterate
+ * (the pair loop's ntheta, :1608-1642 of src/TrigenicInteractionPredictor_23.py), and to nth in
+ * mmsbm_accumulate.  The pointer is read at every launch; it stays set until replaced. */
+int mmsbm_set_theta_addend(mmsbm_ctx *ctx, const double *nth_add);
+
 /* Measurement: info[10] = observations, plan rows (3 streams), stream-0 rows, stream-0
  * workgroups, stream-1/2 workgroups, S-partial workgroups, partial rows, most genes per
  * stream-0 workgroup, V genes over all stream-0 workgroups, stream-0 partial rows. */

@@ -64,6 +64,15 @@ int mmsbm_pairs_set_workspace(mmsbm_pairs_ctx *ctx, void *ws, int64_t bytes);
 int mmsbm_pairs_accumulate(mmsbm_pairs_ctx *ctx, const double *theta, const double *qr, double *nth,
                            double *S2, void *stream);
 
+/* n joint iterations in one call (what JointEngine.iterate runs), all on `stream`.  Per
+ * iteration: one pair launch (pair sums into nth2[B][P][K], scratch, and the S2 partials of its
+ * workgroups), then the triplet iteration of `tri` (mmsbm_iterate) whose fin launch adds nth2
+ * before dividing by the joint counter (mmsbm_set_degree) and, in extra workgroups, sums the
+ * S2 partials and applies the qr M-step: four launches per joint iteration.  `pairs` must have
+ * the same K, R, B and P as `tri`. */
+int mmsbm_joint_iterate(mmsbm_ctx *tri, mmsbm_pairs_ctx *pairs, double *theta, double *pr, double *qr,
+                        double *nth2, int32_t n_iters, void *stream);
+
 /* qr <- qr S2 / (eps + sum_r qr S2) (:1660-1666, :1674-1676). */
 int mmsbm_pairs_qstep(mmsbm_pairs_ctx *ctx, double *qr, const double *S2, void *stream);
 
@@ -77,8 +86,8 @@ int mmsbm_pairs_loglik(mmsbm_pairs_ctx *ctx, int32_t which, const double *theta,
 int mmsbm_pairs_predict(mmsbm_pairs_ctx *ctx, const int32_t *ids, int64_t n, const double *theta,
                         const double *qr, double *out, void *stream);
 
-/* Measurement: info[4] = observations (train), gather entries, gather workgroups,
- * likelihood workgroups of set `which`. */
+/* Measurement: info[7] = observations, gather entries, parts, EM workgroups, most genes and
+ * most parts per EM workgroup (train set), likelihood workgroups of set `which`. */
 int mmsbm_pairs_plan_info(const mmsbm_pairs_ctx *ctx, int32_t which, int64_t *info);
 
 #ifdef __cplusplus

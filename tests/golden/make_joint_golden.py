@@ -104,8 +104,77 @@ def _run_case(ref, case_dir, train, test, K, seed, iters, interaction):
     print("  joint/%s/%s: L_final=%r" % (os.path.basename(case_dir), name, float(out["L_%d" % iters[-1]])))
 
 
+CLI_RUNS = [  # (name, argv of src/trigenic_fromtesttrain_2+3.py without the files, seed)
+    ("v0", [80, 2, 5, 2, 3], 0, 77),
+    ("v1", [400, 2, 10, 2, 0], 1, 78),
+]
+
+
+def _run_driver(ref, case_dir, out_dir):
+    """The loop of src/trigenic_fromtesttrain_2+3.py:65-107 on the reference Model, with the spec
+    fix (likelihoodVector for :78/:86's vlikelihood), seed given instead of os.getpid() (:32).
+    Records stdout and every output file."""
+    import math
+    train, test = os.path.join(case_dir, "train.dat"), os.path.join(case_dir, "test.dat")
+    runs = {}
+    for name, (iterations, samples, fcheck, k, sampleini), verbose, seed in CLI_RUNS:
+        d = os.path.join(out_dir, name)
+        os.makedirs(d, exist_ok=True)
+        cwd = os.getcwd()
+        os.chdir(d)
+        buf = io.StringIO()
+        try:
+            with contextlib.redirect_stdout(buf):
+                random.seed(seed)
+                msg = "\n****************************************\n* Trigenic Interaction Predictor v 1.0 *\n**************"
+                msg += "**************************\n\nDoing " + str(samples) + " samples of " + str(iterations) + " num_iterations."
+                msg += "**************************\n\nStarting from sample " + str(sampleini) + " ."
+                msg += "\nLikelihood will be calculated every " + str(fcheck) + " num_iterations."
+                print(msg)
+                model = ref.Model()
+                model.get_train_test(train, test)
+                print("\nStarting algorithm...")
+                print(verbose)
+                for sample in range(sampleini, sampleini + int(samples)):
+                    print("Sample " + str(1 + sample) + ":")
+                    model.initialize_parameters(k)
+                    print("Parameters have been initialized")
+                    like0 = model.compute_likelihood()
+                    print("· Likelihood 0 is " + str(like0))
+                    model.likelihoodVector.append([sample, 0, like0])
+                    for iteration in range(iterations):
+                        model.make_iteration()
+                        if iteration % fcheck == 0:
+                            like = model.compute_likelihood()
+                            print("· Likelihood " + str(iteration + 1) + " is " + str(like))
+                            model.likelihoodVector.append([sample, iteration + 1, like])
+                            if math.fabs((like - like0) / like0) < 0.001:
+                                print("\n\t****************************\n\t* Likelihood has converged *\n\t****************************")
+                                outfile = 'outSamp%dK%d.csv' % (sample, k)
+                                if verbose == 0:
+                                    model.to_file_short(outfile)
+                                elif verbose == 1:
+                                    model.to_file(outfile)
+                                break
+                            like0 = like
+            files = {f: open(f, encoding="utf-8").read() for f in sorted(os.listdir("."))}
+        finally:
+            os.chdir(cwd)
+        for f in files:
+            os.remove(os.path.join(d, f))
+        os.rmdir(d)
+        runs[name] = {"argv": [str(x) for x in (iterations, samples, fcheck, k, sampleini)] + [verbose, seed],
+                      "stdout": buf.getvalue(), "files": files}
+        print("  joint/cli/%s: files %s" % (name, sorted(files)))
+    with open(os.path.join(out_dir, "driver.json"), "w", encoding="utf-8") as f:
+        json.dump(runs, f, ensure_ascii=False)
+
+
 def main():
     ref = _import_reference()
+    if "--cli-only" in sys.argv:
+        _run_driver(ref, os.path.join(HERE, "joint", "tiny"), os.path.join(HERE, "joint", "cli"))
+        return
     root = os.path.join(HERE, "joint")
     for case, (spec, runs) in CASES.items():
         d = os.path.join(root, case)
@@ -135,6 +204,7 @@ def main():
     with open(os.path.join(root, "zerodeg.json"), "w") as f:
         json.dump({"K": 2, "seed": 9, "P": m.P, "L_0": L0, "raises_zero_division": raised}, f)
     print("  joint/zerodeg: raises=%s" % raised)
+    _run_driver(ref, os.path.join(root, "tiny"), os.path.join(root, "cli"))
 
 
 if __name__ == "__main__":

@@ -74,3 +74,44 @@ class OracleShardEngine:
         if ids.shape[0] == 0:
             return np.zeros(self.B)
         return np.array([c_oracle.loglik(ids, counts, t, p) for t, p in zip(self.theta, self.pr)])
+
+
+class OracleJointEngine:
+    """CPU stand-in for joint.JointEngine on the C oracle's joint iteration (bit-exact with the
+    reference `_23`): lets the joint Model, its text output and cli23 run on the CPU."""
+
+    def __init__(self, K, P, B=1, R=2, eps=1e-10, device=None):
+        self.K, self.P, self.B, self.R, self.eps = K, P, B, R, eps
+        self.sets = {}
+
+    def set_links(self, which, ids3, counts3, ids2, counts2):
+        self.sets[which] = tuple(np.ascontiguousarray(a, dtype=np.int32)
+                                 for a in (np.reshape(ids3, (-1, 3)), np.reshape(counts3, (-1, self.R)),
+                                           np.reshape(ids2, (-1, 2)), np.reshape(counts2, (-1, self.R))))
+
+    def upload(self, theta, pr, qr):
+        self.theta = [np.array(t, dtype=np.float64) for t in theta]
+        self.pr = [np.array(p, dtype=np.float64) for p in pr]
+        self.qr = [np.array(q, dtype=np.float64) for q in qr]
+
+    def download(self):
+        return np.stack(self.theta), np.stack(self.pr), np.stack(self.qr)
+
+    def iterate(self, n=1):
+        for _ in range(int(n)):
+            for s in range(len(self.theta)):
+                self.theta[s], self.pr[s], self.qr[s] = c_oracle.joint_make_iteration(
+                    *self.sets[0], self.theta[s], self.pr[s], self.qr[s])
+
+    def loglik(self, which=0):
+        return np.array([c_oracle.joint_loglik(*self.sets[which], t, p, q)
+                         for t, p, q in zip(self.theta, self.pr, self.qr)])
+
+    def predict(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        f = c_oracle.predict if ids.shape[1] == 3 else c_oracle.pair_predict
+        lat = self.pr if ids.shape[1] == 3 else self.qr
+        return np.stack([f(ids, t, q) for t, q in zip(self.theta, lat)])
+
+    def close(self):
+        pass

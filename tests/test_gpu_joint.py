@@ -198,3 +198,73 @@ def test_joint_batched_samples_and_reproducibility(tmp_path):
     np.testing.assert_array_equal(thR, thB)
     np.testing.assert_array_equal(qrR, qrB)
     np.testing.assert_array_equal(LR, LB)
+
+
+def _lines_close(got, want, rtol=RTOL):
+    """stdout of the driver: every line exact except the likelihood values (rtol)."""
+    g, w = got.split("\n"), want.split("\n")
+    assert len(g) == len(w)
+    for a, b in zip(g, w):
+        if b.startswith("· Likelihood "):
+            ha, va = a.rsplit(" ", 1)
+            hb, vb = b.rsplit(" ", 1)
+            assert ha == hb
+            np.testing.assert_allclose(float(va), float(vb), rtol=rtol)
+        else:
+            assert a == b
+
+
+@pytest.mark.parametrize("name", ["v0", "v1"])
+def test_joint_driver_on_gpu_matches_reference_run(name, tmp_path, monkeypatch, capsys):
+    """cli23 on the HIP engine against the reference's run of src/trigenic_fromtesttrain_2+3.py:
+    same convergence points and files; likelihoods, probabilities and theta / pr / qr text
+    within rtol (to_file) or the to_string_short comparison above."""
+    from trigenicinteractionpredictor_amd import cli23
+    with open(os.path.join(JOINT, "cli", "driver.json"), encoding="utf-8") as f:
+        run = json.load(f)[name]
+    d = os.path.join(JOINT, "tiny")
+    argv = run["argv"][:5] + [os.path.join(d, "train.dat"), os.path.join(d, "test.dat"),
+                              str(run["argv"][5]), str(run["argv"][6])]
+    monkeypatch.chdir(tmp_path)
+    cli23.main(argv)
+    _lines_close(capsys.readouterr().out, run["stdout"])
+    got = {f: open(f, encoding="utf-8").read() for f in sorted(os.listdir("."))}
+    assert sorted(got) == sorted(run["files"])
+    for f, text in got.items():
+        want = run["files"][f]
+        if run["argv"][5] == 0:
+            head = want.split("\n").index("Predicted Interaction\tID of genes\tReal Interaction")
+            end = want.split("\n").index("", head)
+            pred = np.array([float(r.split("\t")[0]) for r in want.split("\n")[head + 1:end]])
+            compare_short(text, want, pred)
+        else:   # to_file: numbers printed with 6 / 12 decimals; compare as numbers
+            for a, b in zip(text.split("\n"), want.split("\n")):
+                fa, fb = a.split("\t"), b.split("\t")
+                assert len(fa) == len(fb)
+                for x, y in zip(fa, fb):
+                    try:
+                        np.testing.assert_allclose(float(x), float(y), rtol=1e-6, atol=2e-12)
+                    except ValueError:
+                        assert x == y
+
+
+def test_joint_fused_and_unfused_paths_agree(tmp_path):
+    """JointEngine.iterate (pair launch + triplet iteration with the theta addend and q cells) against the
+    accumulate / mstep / qstep building blocks: same values within FP64 re-association."""
+    from trigenicinteractionpredictor_amd import _lib
+    from trigenicinteractionpredictor_amd.joint import JointEngine, _pair_arrays
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    m = _joint_fold(tmp_path, P=400, E3=4000, E2=2500, seed=9, pair_only=15)
+    random.seed(3)
+    m.initialize_parameters(12)
+    init = (np.array(m.theta)[None], np.array(m.pr)[None], np.array(m.qr)[None])
+    out = []
+    for mode in ("iterate", "iterate_unfused"):
+        eng = JointEngine(12, m.P, B=1)
+        eng.set_links(_lib.SET_TRAIN, *links_to_arrays(m.links, 2), *_pair_arrays(m.dlinks, 2))
+        eng.upload(*init)
+        getattr(eng, mode)(3)
+        out.append(eng.download())
+        eng.close()
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-300)

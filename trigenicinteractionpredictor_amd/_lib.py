@@ -44,6 +44,7 @@ SIGNATURES = {
     "mmsbm_accumulate": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "mmsbm_mstep": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "mmsbm_plan_info": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i64)]),
+    "mmsbm_set_theta_addend": (_c_int, [_vp, _vp]),
     "mmsbm_timing": (_c_int, [_vp, _c_i32]),
     "mmsbm_timing_result": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_i64)]),
     "mmsbm_time_kernel": (_c_int, [_vp, _c_i32, _vp, _vp, _c_i32, _vp, ctypes.POINTER(_c_dbl)]),
@@ -55,6 +56,7 @@ SIGNATURES = {
     "mmsbm_pairs_workspace_bytes": (_c_int, [_vp, ctypes.POINTER(_c_i64)]),
     "mmsbm_pairs_set_workspace": (_c_int, [_vp, _vp, _c_i64]),
     "mmsbm_pairs_accumulate": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmsbm_joint_iterate": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _c_i32, _vp]),
     "mmsbm_pairs_qstep": (_c_int, [_vp, _vp, _vp, _vp]),
     "mmsbm_pairs_loglik": (_c_int, [_vp, _c_i32, _vp, _vp, _vp, _vp]),
     "mmsbm_pairs_predict": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _vp, _vp]),

@@ -44,6 +44,7 @@
 #include <vector>
 
 #include "mmsbm.h"
+#include "mmsbm_pairs.h"
 #include "plan.h"
 
 namespace {
@@ -677,7 +678,7 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
                                               const double* __restrict__ prows,
                                               const int* __restrict__ prow_ptr, const int* __restrict__ deg,
                                               int P, int R, long long n_prows, double* __restrict__ nth_out,
-                                              double* Ms, Stamp& st_) {
+                                              const double* __restrict__ nth_add, double* Ms, Stamp& st_) {
   using F = FT<K>;
   constexpr int K2 = F::K2, K3 = K * K * K, NGW = F::NGW, NT = F::NT, KP = F::KP;
   const int tid = threadIdx.x, b = blockIdx.y;
@@ -691,6 +692,7 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
   const int eg = tid / K, ex = tid % K;
   const int ge = g0 + eg < P ? g0 + eg : P - 1;
   const double th_e = theta[((size_t)b * P + ge) * K + ex];
+  const double ad_e = nth_add ? nth_add[((size_t)b * P + ge) * K + ex] : 0.0;
   const int deg_e = deg[ge];
   __shared__ int pp[3 * MAX_R][NGW + 1];
   {
@@ -770,6 +772,7 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
     double X = Xr[eg * KP + ex];
 #pragma unroll
     for (int q = 1; q < F::KSPLIT; ++q) X += Xr[(q * NGW + eg) * KP + ex];
+    if (nth_add) X += ad_e;
     const size_t o = ((size_t)b * P + g0 + eg) * K + ex;
     if constexpr (SUMS) nth_out[o] = X;
     else theta[o] = th_e * X / (double)deg_e;
@@ -784,7 +787,8 @@ __global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
     const double* __restrict__ prows, const int* __restrict__ prow_ptr,
     const double* __restrict__ spart, const int* __restrict__ deg, SpRange spr, int P, int R,
     long long n_prows, int n_sp, int n_gene_wg, double eps, double* __restrict__ nth_out,
-    double* __restrict__ S_out) {
+    double* __restrict__ S_out, const double* __restrict__ nth_add,
+    const double* __restrict__ q_part, double* __restrict__ q_out, int n_qwg) {
   using F = FT<K>;
   constexpr int K2 = F::K2, K3 = K * K * K, NG = F::NG;
   extern __shared__ __attribute__((aligned(16))) double Ms[];  // [CB][4 genes][K2P]
@@ -793,7 +797,7 @@ __global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
   st_.mark(0);
   if constexpr (F::GT > 1) {
     if ((int)blockIdx.x < n_gene_wg) {
-      fin_genes_big<K, SUMS>(theta, pold, prows, prow_ptr, deg, P, R, n_prows, nth_out, Ms, st_);
+      fin_genes_big<K, SUMS>(theta, pold, prows, prow_ptr, deg, P, R, n_prows, nth_out, nth_add, Ms, st_);
       return;
     }
   }
@@ -806,11 +810,12 @@ __global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
     double* Ps = Ms + F::MS;  // [R][K3] when F::PLDS
     // epilogue operands (wave 0: gene g0 + hi, x = 4 (4 xg + blk) + lo), loaded up front
     const int ge = g0 + hi < P ? g0 + hi : P - 1;
-    double th_e[F::NXG];
+    double th_e[F::NXG], ad_e[F::NXG];
 #pragma unroll
     for (int xg = 0; xg < F::NXG; ++xg) {
       const int x = 4 * (4 * xg + blk) + lo;
       th_e[xg] = theta[((size_t)b * P + ge) * K + (x < K ? x : 0)];
+      ad_e[xg] = nth_add ? nth_add[((size_t)b * P + ge) * K + (x < K ? x : 0)] : 0.0;
     }
     const int deg_e = deg[ge];
     // partial-row ranges of the 4 genes for every combo (= s * R + r) and p, staged in LDS with
@@ -899,6 +904,7 @@ __global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
         const int x = 4 * (4 * xg + blk) + lo;
         double X = 0.0;
         for (int w = 0; w < 4; ++w) X += Ms[(w * F::NXG + xg) * 64 + lane];
+        if (nth_add) X += ad_e[xg];
         if (g < P && x < K) {
           const size_t o = ((size_t)b * P + g) * K + x;
           if constexpr (SUMS) nth_out[o] = X;
@@ -908,6 +914,51 @@ __global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
     }
     st_.mark(3);
     st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 4 + wv, lane);
+  } else if ((int)blockIdx.x >= n_gene_wg + (K3 + 63) / 64) {
+    // joint model q cells (include/mmsbm_pairs.h): 64 cells of qr per workgroup, NPART threads
+    // per cell each summing a share of the pair launch's S2 partials [B][n_qwg][R][K2] (16 loads
+    // in flight), the shares combined in order; qr <- qr S2 / (eps + sum_r qr S2) (:1660-1666)
+    constexpr int NPART = F::NPART;
+    const int cl = tid & 63, part = tid >> 6;
+    const int cell = (blockIdx.x - n_gene_wg - (K3 + 63) / 64) * 64 + cl;
+    const bool cv = cell < K2;
+    const int cc = cv ? cell : 0;
+    double qo[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) qo[r] = q_out[((size_t)b * R + (r < R ? r : R - 1)) * K2 + cc];
+    const int s0 = n_qwg * part / NPART, s1 = n_qwg * (part + 1) / NPART;
+    for (int r = 0; r < R; ++r) {
+      double S = 0.0;
+      for (int w = s0; w < s1; w += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const double x = q_part[(((size_t)b * n_qwg + (w + u < s1 ? w + u : s0)) * R + r) * K2 + cc];
+          v[u] = w + u < s1 ? x : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) S += v[u];
+      }
+      Ms[(r * NPART + part) * 64 + cl] = S;
+    }
+    __syncthreads();
+    if (part == 0 && cv) {
+      double nq[MAX_R];
+      double den = eps;
+#pragma unroll
+      for (int r = 0; r < MAX_R; ++r) {
+        if (r < R) {
+          double S = Ms[r * NPART * 64 + cl];
+#pragma unroll
+          for (int q = 1; q < NPART; ++q) S += Ms[(r * NPART + q) * 64 + cl];
+          nq[r] = qo[r] * S;
+          den += nq[r];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < MAX_R; ++r)
+        if (r < R) q_out[((size_t)b * R + r) * K2 + cell] = nq[r] / den;
+    }
   } else {
     // 64 cells per workgroup, NPART threads per cell, each summing a share of every rating's S
     // partials (16 loads in flight), the shares combined in order through LDS
@@ -1100,6 +1151,10 @@ struct mmsbm_ctx {
   long long ws_bytes = 0;
   double *cbuf = nullptr, *prows = nullptr, *spart = nullptr, *pold = nullptr, *partL = nullptr;
   double *nth_tmp = nullptr, *S_tmp = nullptr;  // fin_kernel sums-out scratch (kernel timing)
+  const double* nth_add = nullptr;  // joint model: pair sums added before the degree division
+  const double* q_part = nullptr;   // joint model: S2 partials for fin's q cells (null = none)
+  double* q_out = nullptr;          // joint model: qr, updated in place by fin's q cells
+  int n_qwg = 0;                    // joint model: S2 partials per sample
   unsigned attr = 0;             // dynamic-LDS opt-ins done on this context's device
   bool timing = false;
   int timing_stride = 1;
@@ -1215,14 +1270,16 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
     spr.lo[r] = h.sp_lo[r];
     spr.hi[r] = h.sp_hi[r];
   }
+  // joint model: the q cells (qr M-step from the pair launch's S2 partials), theta update only
+  const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
   if (sums)
     fin_kernel<K, true><<<dim3(ngw + ncw, c->B), FT<K>::NT, lds, s>>>(
         theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
-        std::max(h.n_sp, 1), ngw, c->eps, nth, S);
+        std::max(h.n_sp, 1), ngw, c->eps, nth, S, c->nth_add, nullptr, nullptr, 0);
   else
-    fin_kernel<K, false><<<dim3(ngw + ncw, c->B), FT<K>::NT, lds, s>>>(
+    fin_kernel<K, false><<<dim3(ngw + ncw + nqc, c->B), FT<K>::NT, lds, s>>>(
         theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
-        std::max(h.n_sp, 1), ngw, c->eps, nth, S);
+        std::max(h.n_sp, 1), ngw, c->eps, nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -1307,6 +1364,11 @@ int set_degree(mmsbm_ctx* c, const std::vector<int>& deg) {
 }
 
 }  // namespace
+
+// pairs.hip (same library): the fused pair half of a joint iteration and the pair context shape
+int mmsbm_detail_pairs_estep(mmsbm_pairs_ctx* c, const double* theta, const double* qr, double* nth2,
+                             hipStream_t s, const double** s2part, int* n_wg);
+int mmsbm_detail_pairs_shape(const mmsbm_pairs_ctx* c, int* K, int* R, int* B, int* P);
 
 // One error channel for the whole library: pairs.hip (the joint model's pair lattice, same .so)
 // reports through mmsbm_last_error too.
@@ -1608,6 +1670,44 @@ int mmsbm_predict(mmsbm_ctx* c, const int32_t* ids, int64_t n, const double* the
     return fail(MMSBM_ERR_INVALID, "bad arguments");
   DeviceGuard g(c->device);
   return kTable[c->K - 1].predict(c, ids, n, theta, pr, out, (hipStream_t)stream);
+}
+
+// Joint digenic + trigenic iterations (include/mmsbm_pairs.h), all on `stream`: per iteration the
+// pair launch (nth2 and the S2 partials), then pass A, pass B and fin, whose gene part adds nth2
+// before the division by the joint counter and whose q cells sum the S2 partials and update qr.
+int mmsbm_joint_iterate(mmsbm_ctx* c, mmsbm_pairs_ctx* pairs, double* theta, double* pr, double* qr,
+                        double* nth2, int32_t n_iters, void* stream) {
+  if (!c || !pairs) return fail(MMSBM_ERR_INVALID, "null context");
+  int rc = check_ready(c);
+  if (rc) return rc;
+  int pK, pR, pB, pP;
+  mmsbm_detail_pairs_shape(pairs, &pK, &pR, &pB, &pP);
+  if (pK != c->K || pR != c->R || pB != c->B || pP != c->P)
+    return fail(MMSBM_ERR_INVALID, "pair context shape differs from the triplet context");
+  if (c->zero_degree)
+    return fail(MMSBM_ERR_ZERO_DEGREE, "a gene has no train link (float division by zero)");
+  if (!theta || !pr || !qr || !nth2) return fail(MMSBM_ERR_INVALID, "null pointer");
+  if (n_iters < 0) return fail(MMSBM_ERR_INVALID, "n_iters < 0");
+  DeviceGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  const double* keep = c->nth_add;
+  c->nth_add = nth2;
+  c->q_out = qr;
+  for (int it = 0; it < n_iters && rc == MMSBM_OK; ++it) {
+    if ((rc = mmsbm_detail_pairs_estep(pairs, theta, qr, nth2, s, &c->q_part, &c->n_qwg))) break;
+    rc = one_iteration(c, theta, pr, c->timing && it % c->timing_stride == 0, s);
+  }
+  c->nth_add = keep;
+  c->q_part = nullptr;
+  c->q_out = nullptr;
+  c->n_qwg = 0;
+  return rc;
+}
+
+int mmsbm_set_theta_addend(mmsbm_ctx* c, const double* nth_add) {
+  if (!c) return fail(MMSBM_ERR_INVALID, "null context");
+  c->nth_add = nth_add;
+  return MMSBM_OK;
 }
 
 int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {

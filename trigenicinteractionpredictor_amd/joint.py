@@ -130,11 +130,22 @@ class JointEngine:
         return self._torch.cuda.current_stream(self.device).cuda_stream
 
     def iterate(self, n_iters: int = 1):
+        """n joint iterations (mmsbm_joint_iterate): per iteration the pair launch (pair sums,
+        S2 partials), then the triplet iteration whose fin adds the pair sums before the
+        division by the joint counter and applies the qr M-step."""
         if _lib.SET_TRAIN not in self._sets:
             raise RuntimeError("train links not set")
+        _lib.check(self.lib.mmsbm_joint_iterate(self.tri.ctx, self.pctx, self.theta.data_ptr(),
+                                                self.pr.data_ptr(), self.qr.data_ptr(), self.nth.data_ptr(),
+                                                int(n_iters), self._stream()))
+
+    def iterate_unfused(self, n_iters: int = 1):
+        """The same iterations through the accumulate / M-step halves (include/mmsbm_pairs.h):
+        the building blocks a link-sharded joint run would all-reduce between."""
         s = self._stream()
         th, pr, qr = self.theta.data_ptr(), self.pr.data_ptr(), self.qr.data_ptr()
         nth, S, S2 = self.nth.data_ptr(), self.S.data_ptr(), self.S2.data_ptr()
+        _lib.check(self.lib.mmsbm_set_theta_addend(self.tri.ctx, None))
         for _ in range(int(n_iters)):
             _lib.check(self.lib.mmsbm_accumulate(self.tri.ctx, th, pr, nth, S, s))
             _lib.check(self.lib.mmsbm_pairs_accumulate(self.pctx, th, qr, nth, S2, s))
@@ -164,9 +175,10 @@ class JointEngine:
         return out[:, :n].cpu().numpy()
 
     def plan_info(self, which: int = _lib.SET_TRAIN) -> dict:
-        v = (self._ct.c_int64 * 4)()
+        v = (self._ct.c_int64 * 7)()
         _lib.check(self.lib.mmsbm_pairs_plan_info(self.pctx, which, v))
-        info = dict(zip(("pair_observations", "pair_entries", "gather_wgs", "pair_ll_wgs"), [int(x) for x in v]))
+        info = dict(zip(("pair_observations", "pair_entries", "pair_parts", "pair_em_wgs", "pair_wg_genes_max",
+                         "pair_wg_parts_max", "pair_ll_wgs"), [int(x) for x in v]))
         info.update(self.tri.plan_info(which))
         return info
 
@@ -186,6 +198,8 @@ class JointEngine:
 
 class Model:
     """`Model` of src/TrigenicInteractionPredictor_23.py (:37-1697) under the spec fix."""
+
+    Engine = JointEngine   # device engine class (tests substitute a CPU checker engine)
 
     def __init__(self, device=None):
         self.nTheta = []
@@ -253,7 +267,7 @@ class Model:
             if self._engine is not None:
                 self._pull()
                 self._engine.close()
-            eng = JointEngine(self.K, self.P, B=1, R=self.R, eps=self.eps, device=self._device)
+            eng = self.Engine(self.K, self.P, B=1, R=self.R, eps=self.eps, device=self._device)
             eng.set_links(_lib.SET_TRAIN, *links_to_arrays(self.links, self.R), *_pair_arrays(self.dlinks, self.R))
             self._engine = eng
             self._engine_key = key
