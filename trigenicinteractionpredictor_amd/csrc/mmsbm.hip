@@ -595,6 +595,10 @@ struct FT {
                                      : (CB * 4 * K2P > 4 * NXG * 64 ? CB * 4 * K2P : 4 * NXG * 64);
   static constexpr int MS = MS_G > MAX_R * NPART * 64 ? MS_G : MAX_R * NPART * 64;  // doubles
   static constexpr bool PLDS = K <= 12;  // p of every rating staged in LDS (else read from L2)
+  // cell part: CL rounds of 64 cells per workgroup (CL = 8 at K = 20 x 8 samples measured slower:
+  // fin 221 -> 244 us, the longer cell workgroups finish last)
+  static constexpr int CL = 1;
+  static constexpr int NCW = (K * K * K + 64 * CL - 1) / (64 * CL);
   static constexpr int LDS = (MS + (PLDS ? MAX_R * K * K * K : 0)) * 8;
   static_assert(GT == 1 || NXG * KSPLIT == 8, "big fin: one (x group, k part) per wave");
   static_assert(GT == 1 || NGW * K <= NT, "big fin epilogue: one (gene, x) per thread");
@@ -914,13 +918,13 @@ __global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
     }
     st_.mark(3);
     st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 4 + wv, lane);
-  } else if ((int)blockIdx.x >= n_gene_wg + (K3 + 63) / 64) {
+  } else if ((int)blockIdx.x >= n_gene_wg + F::NCW) {
     // joint model q cells (include/mmsbm_pairs.h): 64 cells of qr per workgroup, NPART threads
     // per cell each summing a share of the pair launch's S2 partials [B][n_qwg][R][K2] (16 loads
     // in flight), the shares combined in order; qr <- qr S2 / (eps + sum_r qr S2) (:1660-1666)
     constexpr int NPART = F::NPART;
     const int cl = tid & 63, part = tid >> 6;
-    const int cell = (blockIdx.x - n_gene_wg - (K3 + 63) / 64) * 64 + cl;
+    const int cell = (blockIdx.x - n_gene_wg - F::NCW) * 64 + cl;
     const bool cv = cell < K2;
     const int cc = cv ? cell : 0;
     double qo[MAX_R];
@@ -960,11 +964,15 @@ __global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
         if (r < R) q_out[((size_t)b * R + r) * K2 + cell] = nq[r] / den;
     }
   } else {
-    // 64 cells per workgroup, NPART threads per cell, each summing a share of every rating's S
-    // partials (16 loads in flight), the shares combined in order through LDS
+    // CL rounds of 64 cells per workgroup, NPART threads per cell, each summing a share of every
+    // rating's S partials (16 loads in flight), the shares combined in order through LDS
     constexpr int NPART = F::NPART;
     const int cl = tid & 63, part = tid >> 6;
-    const int cell = (blockIdx.x - n_gene_wg) * 64 + cl;
+    for (int sub = 0; sub < F::CL; ++sub) {
+    const int cb0 = ((blockIdx.x - n_gene_wg) * F::CL + sub) * 64;
+    if (cb0 >= K3) break;  // uniform over the workgroup
+    if (sub > 0) __syncthreads();  // the previous round's reads of Ms are done
+    const int cell = cb0 + cl;
     const bool cv = cell < K3;
     const int cc = cv ? cell : 0;
     double po[MAX_R];
@@ -1009,6 +1017,7 @@ __global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
         for (int r = 0; r < MAX_R; ++r)
           if (r < R) pr[((size_t)b * R + r) * K3 + cell] = npr[r] / den;
       }
+    }
     }
   }
 }
@@ -1260,7 +1269,7 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   const SetDev& sd = c->sets[MMSBM_SET_TRAIN];
   const auto& h = sd.h;
   const int ngw = (c->P + FT<K>::NGW - 1) / FT<K>::NGW;
-  const int ncw = (T::K3 + 63) / 64;
+  const int ncw = FT<K>::NCW;
   int rc;
   if ((rc = lds_opt_in(c, sums ? 3 : 2, sums ? &fin_kernel<K, true> : &fin_kernel<K, false>, FT<K>::LDS)))
     return rc;
