@@ -268,3 +268,29 @@ def test_joint_fused_and_unfused_paths_agree(tmp_path):
         eng.close()
     for a, b in zip(out[0], out[1]):
         np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-300)
+
+
+def test_joint_plan_splits_agree(tmp_path, monkeypatch):
+    """Small pair workgroups (MMSBM_PAIR_PARTS=16: many workgroups, every gene block split
+    differently) give the same iteration as the default plan, up to the S2 re-association."""
+    from trigenicinteractionpredictor_amd import _lib
+    from trigenicinteractionpredictor_amd.joint import JointEngine, _pair_arrays
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    m = _joint_fold(tmp_path, P=300, E3=2500, E2=3000, seed=11, pair_only=20)
+    random.seed(4)
+    m.initialize_parameters(9)
+    init = (np.array(m.theta)[None], np.array(m.pr)[None], np.array(m.qr)[None])
+    out = []
+    for parts in (None, "16"):
+        if parts:
+            monkeypatch.setenv("MMSBM_PAIR_PARTS", parts)
+        eng = JointEngine(9, m.P, B=1)
+        eng.set_links(_lib.SET_TRAIN, *links_to_arrays(m.links, 2), *_pair_arrays(m.dlinks, 2))
+        if parts:
+            assert eng.plan_info(0)["pair_wg_parts_max"] <= 16 * 4
+        eng.upload(*init)
+        eng.iterate(3)
+        out.append(eng.download())
+        eng.close()
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-300)

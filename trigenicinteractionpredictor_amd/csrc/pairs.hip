@@ -31,6 +31,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <utility>
 #include <vector>
 
@@ -354,9 +355,9 @@ struct PairSet {
 };
 
 // plan constants: a run is split into parts of >= 8 entries, at most 32 parts; a workgroup takes
-// whole genes while it has <= GW(K) genes and <= 256 parts (a lone gene may exceed the part cap:
+// whole genes while it has <= GW(K) genes and <= 64 parts (a lone gene may exceed the part cap:
 // the part loop strides by the workgroup size)
-constexpr int PART_MIN = 8, PART_MAX = 32, WG_PARTS = 256;
+constexpr int PART_MIN = 8, PART_MAX = 32, WG_PARTS = 64;  // 64: sweep in DESIGN.md
 constexpr int gather_wg_genes(int K) { return K <= 16 ? 64 : 32; }
 
 }  // namespace
@@ -490,6 +491,11 @@ const auto kPTable = make_table(std::make_integer_sequence<int, MMSBM_MAX_K>{});
 // Train plan: entries by (gene, slot, rating) run, parts, workgroups of whole genes.
 int build_train_plan(mmsbm_pairs_ctx* c, PairSet& ps, const std::vector<int4>& obs) {
   const int R = c->R, NR = 2 * R, P = c->P, GW = gather_wg_genes(c->K);
+  int wg_parts = WG_PARTS;  // MMSBM_PAIR_PARTS=n: parts per workgroup (measurement sweeps)
+  if (const char* e = getenv("MMSBM_PAIR_PARTS")) {
+    const int v = atoi(e);
+    if (v >= 16 && v <= 1024) wg_parts = v;
+  }
   const size_t nrun = (size_t)P * NR;
   std::vector<int> run_ptr(nrun + 1, 0);
   for (const int4& o : obs) {
@@ -522,7 +528,7 @@ int build_train_plan(mmsbm_pairs_ctx* c, PairSet& ps, const std::vector<int4>& o
     int np = 0;
     while (g < P) {
       const int gp = run_part_ptr[(size_t)(g + 1) * NR] - run_part_ptr[(size_t)g * NR];
-      if (g > g0 && (g - g0 >= GW || np + gp > WG_PARTS)) break;
+      if (g > g0 && (g - g0 >= GW || np + gp > wg_parts)) break;
       np += gp;
       ++g;
     }
