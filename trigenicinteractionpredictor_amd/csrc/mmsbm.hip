@@ -84,8 +84,6 @@ struct KT {
   static constexpr int KP = 4 * NG;
   static constexpr int K2 = K * K, K3 = K * K * K;
   static constexpr int NBG = (NG + 3) / 4;        // Z phase: groups of 4 b-tiles (one per block)
-  static constexpr int NGB = (NG + 3) / 4;        // M phase: groups of 4 y tiles (one per block)
-  static constexpr int NTS = NG * NGB;            // M phase steps: x tile ts / NGB, y tiles 4 (ts % NGB) + blk
   static constexpr int VROWS = 16 * NBG;          // V image rows (b); zero from K on
   static constexpr int VR = KP + 2;               // row stride: 2 x odd doubles, conflict-free B reads
   static constexpr int VDBL = VROWS * VR;         // one gene's V image
@@ -111,6 +109,13 @@ int gmax_for(int K);  // host view of KT<K>::GMAX (table below)
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// v_mfma_f64_16x16x4_f64: lane l holds A[l & 15][l >> 4], B[l >> 4][l & 15]; D[(l >> 4) + 4 i][l & 15]
+// in element i (MI355X guide: the f64 C/D map differs from the f32 one)
+typedef double d4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ d4v mfma16(double a, double b, d4v c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
 // Stores of the per-iteration intermediates (c, partial rows, S partials, the p snapshot) write
@@ -447,9 +452,10 @@ __global__ __launch_bounds__(NT) void pass_kernel(
       *reinterpret_cast<SV*>(soff[t] >= 0 ? I + soff[t] : dummy) = v[t];
   };
 
-  double macc[T::NTS];
+  constexpr int NX16 = (K + 15) / 16;  // 16-wide tiles of each M axis
+  d4v m16[NX16 * NX16];
 #pragma unroll
-  for (int t = 0; t < T::NTS; ++t) macc[t] = 0.0;
+  for (int t = 0; t < NX16 * NX16; ++t) m16[t] = d4v{0.0, 0.0, 0.0, 0.0};
   double ll = 0.0;
   // the image's pad columns are read (times a zero Z entry) by the d dot product: keep them 0
   for (int idx = lane; idx < 2 * T::IMG; idx += 64) img[idx] = 0.0;
@@ -510,29 +516,39 @@ __global__ __launch_bounds__(NT) void pass_kernel(
           }
         }
         if constexpr (MODE != PASS_LL) {
-          // ---- M += c th_u (x) th_v over the chunk's 4 observations
-          // step ts: x tile ts / NGB (the same in every block), y tile 4 (ts % NGB) + blk, so a
-          // lane reads NG A values and NGB B values per chunk
-          // c_o scales the B side (NGB values per lane instead of NG)
-          double au[NG], bvv[T::NGB];
+          // ---- M += c th_u (x) th_v over the chunk's 4 observations: one v_mfma_f64_16x16x4 per
+          // 16 x 16 tile of M, k = the 4 observations.  Lane l holds A[x = l & 15][o = l >> 4] =
+          // th_u(obs hi)[x] and B[o = l >> 4][y = l & 15] = c_hi th_v(obs hi)[y]: both come from
+          // this lane's own observation hi, whose c it already holds; D[x = hi + 4 i][y = l & 15]
+          // in accumulator element i.
+          const int col = lane & 15;
+          double a16[NX16], b16[NX16];
 #pragma unroll
-          for (int xs = 0; xs < NG; ++xs) au[xs] = I[hi * TR + 4 * xs + lo];
-#pragma unroll
-          for (int j = 0; j < T::NGB; ++j) {
-            const int ys = 4 * j + blk;
-            const double v = I[(4 + hi) * TR + (ys < NG ? 4 * ys + lo : 0)];
-            bvv[j] = ys < NG ? c * v : 0.0;
+          for (int t = 0; t < NX16; ++t) {
+            const int x = 16 * t + col;
+            const bool ok = x < K;
+            const double va = I[hi * TR + (ok ? x : 0)];
+            const double vb = I[(4 + hi) * TR + (ok ? x : 0)];
+            a16[t] = ok ? va : 0.0;
+            b16[t] = ok ? c * vb : 0.0;
           }
 #pragma unroll
-          for (int ts = 0; ts < T::NTS; ++ts) macc[ts] = mfma4(au[ts / T::NGB], bvv[ts % T::NGB], macc[ts]);
+          for (int tx = 0; tx < NX16; ++tx)
+#pragma unroll
+            for (int ty = 0; ty < NX16; ++ty)
+              m16[tx * NX16 + ty] = mfma16(a16[tx], b16[ty], m16[tx * NX16 + ty]);
           if (q + 1 >= c1 || pr1 != pr0) {  // end of this gene stretch: its partial row
             double* __restrict__ out = pb + (size_t)pr0 * T::K2;
 #pragma unroll
-            for (int ts = 0; ts < T::NTS; ++ts) {
-              const int x = 4 * (ts / T::NGB) + hi, y = 4 * (4 * (ts % T::NGB) + blk) + lo;
-              if (x < K && y < K) st_wt(out + x * K + y, macc[ts]);
-              macc[ts] = 0.0;
-            }
+            for (int tx = 0; tx < NX16; ++tx)
+#pragma unroll
+              for (int ty = 0; ty < NX16; ++ty)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const int x = 16 * tx + hi + 4 * i, y = 16 * ty + col;
+                  if (x < K && y < K) st_wt(out + x * K + y, m16[tx * NX16 + ty][i]);
+                  m16[tx * NX16 + ty][i] = 0.0;
+                }
           }
         }
         // next chunk's image into the other buffer (its reads of this buffer are done)
