@@ -246,3 +246,38 @@ def test_empty_test_set(tmp_path):
     m.initialize_parameters(2)
     m.make_iteration()
     assert m.compute_likelihood("test") == 0.0
+
+
+@pytest.mark.parametrize("G", [1, 3, 8])
+def test_graph_replay_matches_direct_launches_bitwise(tmp_path, monkeypatch, G):
+    """MMSBM_GRAPH=G replays G iterations per hipGraph launch: the same kernels with the same
+    arguments, so the bits equal direct launches; a new link set (context generation) or new
+    theta / p buffers re-capture the graph."""
+    from trigenicinteractionpredictor_amd import EMEngine, Model
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    tr, te = _fold(tmp_path, 300, 5000, seed=11)
+    m = Model()
+    m.get_traintest(tr, te)
+    K, B = 10, 2
+    random.seed(3)
+    thetas, prs = [], []
+    for _ in range(B):
+        m.initialize_parameters(K)
+        thetas.append(np.array(m.theta))
+        prs.append(np.array(m.pr))
+    ids, counts = links_to_arrays(m.links)
+    out = {}
+    for mode in ("0", str(G)):
+        monkeypatch.setenv("MMSBM_GRAPH", mode)
+        eng = EMEngine(K, m.P, B=B)
+        eng.set_links(0, ids, counts)
+        eng.upload(np.stack(thetas), np.stack(prs))
+        eng.iterate(2 * G + 2)            # warm-up iteration, two graph launches, remainder
+        eng.iterate(G)
+        first = eng.download()
+        eng.set_links(0, ids[::-1].copy(), counts[::-1].copy())   # new plan: re-capture
+        eng.iterate(G + 1)
+        out[mode] = (first, eng.download())
+    for a, b in zip(out["0"], out[str(G)]):
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])

@@ -1185,6 +1185,17 @@ struct mmsbm_ctx {
   int timing_stride = 1;
   std::vector<hipEvent_t> ev[3];
   size_t nev[3] = {0, 0, 0};
+  // hipGraph replay of mmsbm_iterate (MMSBM_GRAPH=G: G iterations per graph, 0 = direct launches).
+  // The graph bakes in every kernel argument, so each setter bumps `gen` and a stale graph is
+  // re-captured.
+  int graph_iters = 0;
+  unsigned long long gen = 1;
+  bool warm = false;                 // a direct iteration ran (LDS opt-ins done before capture)
+  hipStream_t cap = nullptr;         // capture stream (torch's default stream cannot be captured)
+  hipGraphExec_t gexec = nullptr;
+  const double *g_theta = nullptr, *g_pr = nullptr;
+  unsigned long long g_gen = 0;
+  int g_iters = 0;
 };
 
 namespace {
@@ -1377,6 +1388,7 @@ int upload(D** dst, const std::vector<T>& src) {
 }
 
 int set_degree(mmsbm_ctx* c, const std::vector<int>& deg) {
+  ++c->gen;
   c->deg_host = deg;
   c->zero_degree = false;
   for (int v : deg)
@@ -1416,6 +1428,7 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
     return fail(MMSBM_ERR_INVALID, "device %d outside [0, %d)", device, ndev);
   auto* c = new mmsbm_ctx();
   c->device = device;
+  if (const char* gi = getenv("MMSBM_GRAPH")) c->graph_iters = std::max(0, atoi(gi));
   if (MMSBM_STAMP && getenv("MMSBM_STAMP")) {
     DeviceGuard g(device);
     const size_t bytes = sizeof(unsigned long long) * 5 * STAMP_WAVES * STAMP_SLOTS;
@@ -1433,6 +1446,8 @@ int mmsbm_destroy(mmsbm_ctx* c) {
   for (auto& s : c->sets) s.release();
   if (c->deg) (void)hipFree(c->deg);
   if (c->stamp) (void)hipFree(c->stamp);
+  if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+  if (c->cap) (void)hipStreamDestroy(c->cap);
   for (auto& v : c->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   delete c;
@@ -1452,6 +1467,7 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
   c->B = B;
   c->P = P;
   c->eps = eps;
+  ++c->gen;
   // genes per stream-0 workgroup: the LDS budget's GMAX; MMSBM_GCAP=n lowers it (measurement:
   // smaller V tables let more workgroups share a CU)
   c->gcap = gmax_for(K);
@@ -1514,6 +1530,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   if ((rc = upload(&sd.prow_gene, h.prow_gene))) return rc;
   if ((rc = upload(&sd.sp_desc, h.sp_desc))) return rc;
   sd.present = true;
+  ++c->gen;
   c->ws = nullptr;  // the workspace layout changed: mmsbm_set_workspace again
   if (em) {
     if (!c->deg_override) {
@@ -1549,6 +1566,7 @@ int mmsbm_set_workspace(mmsbm_ctx* c, void* ws, int64_t bytes) {
   DeviceGuard g(c->device);
   c->ws = (char*)ws;
   c->ws_bytes = bytes;
+  ++c->gen;
   c->cbuf = (double*)(c->ws + L.cbuf);
   c->prows = (double*)(c->ws + L.prows);
   c->spart = (double*)(c->ws + L.spart);
@@ -1576,6 +1594,40 @@ static int one_iteration(mmsbm_ctx* c, double* theta, double* pr, bool mark, hip
   if (mark && (rc = timing_mark(c, 2, s))) return rc;
   if ((rc = L.fin(c, false, theta, pr, nullptr, nullptr, s))) return rc;
   if (mark && (rc = timing_mark(c, 2, s))) return rc;
+  c->warm = true;
+  return MMSBM_OK;
+}
+
+// G iterations as one hipGraph launch on s (captured once per theta / pr / context generation).
+static int graph_iterations(mmsbm_ctx* c, double* theta, double* pr, int G, hipStream_t s) {
+  if (!c->gexec || c->g_theta != theta || c->g_pr != pr || c->g_gen != c->gen || c->g_iters != G) {
+    if (c->gexec) {
+      HIP_TRY(hipGraphExecDestroy(c->gexec));
+      c->gexec = nullptr;
+    }
+    if (!c->cap) HIP_TRY(hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking));
+    HIP_TRY(hipStreamBeginCapture(c->cap, hipStreamCaptureModeRelaxed));
+    int rc = MMSBM_OK;
+    for (int i = 0; i < G && rc == MMSBM_OK; ++i) rc = one_iteration(c, theta, pr, false, c->cap);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->cap, &g);
+    if (rc == MMSBM_OK && e != hipSuccess)
+      rc = fail(MMSBM_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+    if (rc == MMSBM_OK) {
+      const hipError_t ei = hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0);
+      if (ei != hipSuccess) {
+        c->gexec = nullptr;
+        rc = fail(MMSBM_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+      }
+    }
+    if (g) (void)hipGraphDestroy(g);
+    if (rc) return rc;
+    c->g_theta = theta;
+    c->g_pr = pr;
+    c->g_gen = c->gen;
+    c->g_iters = G;
+  }
+  HIP_TRY(hipGraphLaunch(c->gexec, s));
   return MMSBM_OK;
 }
 
@@ -1589,7 +1641,17 @@ int mmsbm_iterate(mmsbm_ctx* c, double* theta, double* pr, int32_t n_iters, void
   if (n_iters < 0) return fail(MMSBM_ERR_INVALID, "n_iters < 0");
   DeviceGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
-  for (int it = 0; it < n_iters; ++it)
+  int it = 0;
+  const int G = c->graph_iters;
+  if (G > 0 && !c->timing && !c->stamp) {
+    if (!c->warm && n_iters > 0) {
+      if ((rc = one_iteration(c, theta, pr, false, s))) return rc;
+      ++it;
+    }
+    for (; n_iters - it >= G; it += G)
+      if ((rc = graph_iterations(c, theta, pr, G, s))) return rc;
+  }
+  for (; it < n_iters; ++it)
     if ((rc = one_iteration(c, theta, pr, c->timing && it % c->timing_stride == 0, s))) return rc;
   if (c->stamp && n_iters > 0) {  // measurement: phase cycles of the last iteration's waves
     std::vector<unsigned long long> h((size_t)5 * STAMP_WAVES * STAMP_SLOTS);
@@ -1732,6 +1794,7 @@ int mmsbm_joint_iterate(mmsbm_ctx* c, mmsbm_pairs_ctx* pairs, double* theta, dou
 int mmsbm_set_theta_addend(mmsbm_ctx* c, const double* nth_add) {
   if (!c) return fail(MMSBM_ERR_INVALID, "null context");
   c->nth_add = nth_add;
+  ++c->gen;
   return MMSBM_OK;
 }
 
