@@ -399,6 +399,9 @@ def main():
             "iteration": {"us": iter_s * 1e6,
                           "s8d_credit_flops": s8d_flops,
                           "s8d_effective_tflops": s8d_flops / iter_s / 1e12,
+                          # the same credit against the FP64 MFMA peak (SURVEY 8d's binding
+                          # roof for K >= 3): whole iteration, all three kernels
+                          "s8d_frac": s8d_flops / iter_s / 1e12 / FP64_PEAK_TFLOPS,
                           "note": "SURVEY 8d credits 8 K^3 FLOPs per observation (the reference's "
                                   "per-link lattice); the pivot-run factorisation executes "
                                   "O(K^2) per observation + O(K^3) per gene (DESIGN.md)"},

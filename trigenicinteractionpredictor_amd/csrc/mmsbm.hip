@@ -76,7 +76,11 @@ int fail(int code, const char* fmt, ...) {
 // ------------------------------------------------------------------------------------------
 // Compile-time shape of one K.
 // ------------------------------------------------------------------------------------------
-constexpr int lds_target(int K) { return K <= 16 ? 76 * 1024 : 150 * 1024; }
+// Pass-A LDS budget (V tables of GMAX genes + the wave images): two workgroups per CU at every K.
+// Measured (tools/gpu_r02c_gcap.sh): a 150 KB budget (one workgroup per CU, GMAX 22 at K = 20,
+// 13 at K = 30) ran pass A at 156 us (K = 20 x 8) and 2088 us (K = 30, 10M links); 78 KB
+// (GMAX 9 / 4) at 125 us and 1794 us.
+constexpr int lds_target(int K) { return K <= 16 ? 76 * 1024 : 78 * 1024; }
 
 template <int K>
 struct KT {
@@ -380,21 +384,26 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     // wave wv owns cell groups (4 cell tiles) cg = wv, wv + NW, ..., CPR per round, for every
     // gene tile: each p value is loaded once and feeds GT MFMAs (A = the tile's theta rows)
     constexpr int CPR = K <= 12 ? 1 : 2;
-    for (int c0 = wv; c0 < CG; c0 += CPR * NW) {
-      double bv[CPR][NG];
-      int ctv[CPR];
+    // software pipeline over the rounds: the next round's p values (from L2 when K > 12) are in
+    // flight during this round's MFMAs; every load is unconditional (clamped address, value
+    // selected afterwards), a round past the last cell group only loads
+    auto v_load = [&](int cr, double (&bv)[CPR][NG], int (&ctv)[CPR]) {
 #pragma unroll
       for (int u = 0; u < CPR; ++u) {
-        const int ct = 4 * (c0 + u * NW) + blk;
-        const bool cv = c0 + u * NW < CG && ct < CT;
+        const int ct = 4 * (cr + u * NW) + blk;
+        const bool cv = cr + u * NW < CG && ct < CT;
         const int bb = cv ? ct / NG : 0, hh = cv ? 4 * (ct % NG) + lo : 0;
         ctv[u] = cv ? ct : -1;
 #pragma unroll
         for (int as = 0; as < NG; ++as) {
           const int a = 4 * as + hi;
-          bv[u][as] = (cv && a < K && hh < K) ? pv_src[(a * K + bb) * K + hh] : 0.0;
+          const bool ok = cv && a < K && hh < K;
+          const double v = pv_src[ok ? (a * K + bb) * K + hh : 0];
+          bv[u][as] = ok ? v : 0.0;
         }
       }
+    };
+    auto v_round = [&](const double (&bv)[CPR][NG], const int (&ctv)[CPR]) {
 #pragma unroll
       for (int u = 0; u < CPR; ++u) {
         double acc[GTM];
@@ -412,6 +421,16 @@ __global__ __launch_bounds__(NT) void pass_kernel(
           if (t < GT && ct >= 0 && go < ng) Vt[go * T::VDBL + (ct / NG) * VR + 4 * (ct % NG) + lo] = acc[t];
         }
       }
+    };
+    constexpr int CST = CPR * NW;  // cell groups per round (all waves)
+    double bvA[CPR][NG], bvB[CPR][NG];
+    int ctA[CPR], ctB[CPR];
+    v_load(wv, bvA, ctA);
+    for (int cr = wv; cr < CG; cr += 2 * CST) {
+      v_load(cr + CST, bvB, ctB);
+      v_round(bvA, ctA);
+      v_load(cr + 2 * CST, bvA, ctA);
+      if (cr + CST < CG) v_round(bvB, ctB);
     }
     __syncthreads();
   }
