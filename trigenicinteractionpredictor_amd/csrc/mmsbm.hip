@@ -635,6 +635,12 @@ struct FT {
   static constexpr int CL = 1;
   static constexpr int NCW = (K * K * K + 64 * CL - 1) / (64 * CL);
   static constexpr int LDS = (MS + (PLDS ? MAX_R * K * K * K : 0)) * 8;
+  // big fin whose LDS lets two workgroups share a CU (K = 20-23): rounds of 6 partial-row entries
+  // and a 128-VGPR budget (4 waves per SIMD; no spills there, K = 14-19 would spill 8-23); above,
+  // LDS allows one workgroup and 12 entries per round keep more loads in flight
+  static constexpr bool TWO = GT > 1 && 2 * LDS <= 160 * 1024 && K >= 20;
+  static constexpr int RE_CAP = TWO ? 6 : 12;
+  static constexpr int WPE = TWO ? 4 : 1;
   static_assert(GT == 1 || NXG * KSPLIT == 8, "big fin: one (x group, k part) per wave");
   static_assert(GT == 1 || NGW * K <= NT, "big fin epilogue: one (gene, x) per thread");
   static_assert(LDS <= 160 * 1024, "fin LDS over budget");
@@ -746,7 +752,7 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
 #pragma unroll
   for (int t = 0; t < F::GT; ++t) acc[t] = 0.0;
   constexpr int NE = NGW * F::K2P;
-  constexpr int NEPT = (NE + NT - 1) / NT, RE = NEPT < 12 ? NEPT : 12;
+  constexpr int NEPT = (NE + NT - 1) / NT, RE = NEPT < F::RE_CAP ? NEPT : F::RE_CAP;
   // one round of RE entries per thread: each entry's first two partial rows loaded with the whole
   // round in flight (addresses clamped, loads unconditional); the first round of the next combo
   // is loaded before this combo's contraction, so its latency hides under the MFMAs.  Only the
@@ -821,7 +827,7 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
 }
 
 template <int K, bool SUMS>
-__global__ __launch_bounds__(FT<K>::NT) void fin_kernel(
+__global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>::WPE))) void fin_kernel(
     double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ pold,
     const double* __restrict__ prows, const int* __restrict__ prow_ptr,
     const double* __restrict__ spart, const int* __restrict__ deg, SpRange spr, int P, int R,
