@@ -281,3 +281,37 @@ def test_graph_replay_matches_direct_launches_bitwise(tmp_path, monkeypatch, G):
     for a, b in zip(out["0"], out[str(G)]):
         np.testing.assert_array_equal(a[0], b[0])
         np.testing.assert_array_equal(a[1], b[1])
+
+
+def test_context_reshaped_to_another_K_matches_oracle(tmp_path):
+    """mmsbm_set_shape on a used context (K=10 -> K=20): the >64 KB dynamic-LDS opt-ins belong to
+    the kernels of the new K, so they are redone, and the iteration matches the C oracle."""
+    import torch
+    from oracle import c_oracle
+    from trigenicinteractionpredictor_amd import EMEngine, Model, _lib
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    tr, te = _fold(tmp_path, 300, 5000, seed=21)
+    m = Model()
+    m.get_traintest(tr, te)
+    ids, counts = links_to_arrays(m.links)
+    random.seed(4)
+    m.initialize_parameters(10)
+    eng = EMEngine(10, m.P)
+    eng.set_links(0, ids, counts)
+    eng.upload(np.array(m.theta)[None], np.array(m.pr)[None])
+    eng.iterate(1)
+    m.initialize_parameters(20)
+    th0, pr0 = np.array(m.theta), np.array(m.pr)
+    _lib.check(eng.lib.mmsbm_set_shape(eng.ctx, 20, 2, 1, m.P, 1e-10))
+    eng.K, eng.K3 = 20, 20 ** 3
+    eng.theta = torch.zeros((1, m.P, 20), dtype=torch.float64, device=eng.device)
+    eng.pr = torch.zeros((1, 2, 20 ** 3), dtype=torch.float64, device=eng.device)
+    eng.set_links(0, ids, counts)
+    eng.upload(th0[None], pr0[None])
+    eng.iterate(2)
+    th, pr = eng.download()
+    th_o, pr_o = th0, pr0
+    for _ in range(2):
+        th_o, pr_o = c_oracle.make_iteration(ids, counts, th_o, pr_o)
+    np.testing.assert_allclose(th[0], th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(pr[0], pr_o, rtol=RTOL, atol=ATOL)

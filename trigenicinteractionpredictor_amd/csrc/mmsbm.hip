@@ -1493,6 +1493,8 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
   c->P = P;
   c->eps = eps;
   ++c->gen;
+  c->attr = 0;      // the dynamic-LDS opt-ins are per kernel, and the kernels depend on K
+  c->warm = false;
   // genes per stream-0 workgroup: the LDS budget's GMAX; MMSBM_GCAP=n lowers it (measurement:
   // smaller V tables let more workgroups share a CU)
   c->gcap = gmax_for(K);
