@@ -129,6 +129,73 @@ def kernel_work(plan, K, P, R, B, E_obs):
     return {"pass_a": (a_fl * B, a_by * B), "pass_b": (b_fl * B, b_by * B), "fin": (f_fl * B, f_by * B)}
 
 
+def s8d_work(K, P, R, B, E_obs):
+    """SURVEY.md 8d's algorithmic work of one EM iteration of B samples: F = 8 K^3 per observed
+    (link, r) (the reference's lattice) + the M-step 2 P K + 3 K^3 R, and the compulsory HBM
+    bytes B_hbm = 16 E_obs + 2 * 8 P K + 3 * 8 K^3 R (records once, theta read + written,
+    p / S)."""
+    flops = (8.0 * K ** 3 * E_obs + 2.0 * P * K + 3.0 * K ** 3 * R) * B
+    hbm = (16.0 * E_obs + 16.0 * P * K + 24.0 * K ** 3 * R) * B
+    return flops, hbm
+
+
+def pmc_traffic(build_id, K, E_obs, B):
+    """HBM bytes per launch / per iteration from a PMC record under profiles/ taken with THIS
+    build (tools/pmc_to_traffic.py stamps each record with the profiled library's build id);
+    None when no record names this build."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
+        try:
+            with open(f) as fh:
+                rec = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if (rec.get("build_id") == build_id and rec.get("K") == K and rec.get("E_obs") == E_obs
+                and rec.get("B") == B and rec.get("hbm_bytes_per_launch")):
+            best = (os.path.relpath(f, REPO), rec)
+    return best
+
+
+def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
+    """The bench line's `roofline` (DESIGN.md "Roofline accounting").  Headline: SURVEY 8d's
+    binding roof for K >= 3, FP64: achieved = 8d FLOPs of one iteration / the measured iteration
+    time (the timed region), against the FP64 MFMA peak.  Beside it: the FLOPs the engine really
+    executes (its factorisation does far fewer), the 8d compulsory HBM bytes against the HBM
+    peak, and the longest kernel of the iteration timed alone back to back with HIP events."""
+    f8, b8 = s8d_work(K, P, R, B, E_obs)
+    work = kernel_work(plan, K, P, R, B, E_obs)
+    exe = sum(fl for fl, _ in work.values())
+    tf = f8 / iter_s / 1e12
+    dom = max(b2b, key=b2b.get)
+    dom_s = b2b[dom] / 1e3
+    dfl, dby = work[dom]
+    pmc = pmc_traffic(build_id, K, E_obs, B)
+    traffic = None
+    if pmc is not None:
+        traffic = sum(pmc[1]["hbm_bytes_per_launch"].get(k, 0.0) for k in work)
+    return {"bound": "mfma", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": tf / FP64_PEAK_TFLOPS,
+            "traffic": traffic,
+            "traffic_unit": "HBM bytes per iteration (PMC FETCH_SIZE x 2 + WRITE_SIZE, all kernels)",
+            "traffic_source": None if pmc is None else pmc[0],
+            "traffic_build_id": None if pmc is None else pmc[1]["build_id"],
+            "per": "one EM iteration of all %d sample(s): %.4g FLOPs credited by SURVEY 8d "
+                   "(8 K^3 per observation + the M-step) / %.3f us measured" % (B, f8, iter_s * 1e6),
+            "credited_flops_per_iteration": f8,
+            "executed": {"flops_per_iteration": exe, "achieved": exe / iter_s / 1e12,
+                         "peak": FP64_PEAK_TFLOPS, "frac": exe / iter_s / 1e12 / FP64_PEAK_TFLOPS},
+            "hbm": {"bytes_per_iteration": b8, "achieved": b8 / iter_s / 1e9, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": b8 / iter_s / 1e9 / HBM_PEAK_GBS,
+                    "traffic_over_compulsory": None if traffic is None else traffic / b8},
+            "dominant_kernel": {"kernel": KERNEL_NAMES[dom] % K, "avg_launch_us": dom_s * 1e6,
+                                "executed_flops_per_launch": dfl, "algorithmic_bytes_per_launch": dby,
+                                "tflops": dfl / dom_s / 1e12, "mfma_frac": dfl / dom_s / 1e12 / FP64_PEAK_TFLOPS,
+                                "gbs": dby / dom_s / 1e9, "hbm_frac": dby / dom_s / 1e9 / HBM_PEAK_GBS,
+                                "traffic_per_launch": None if pmc is None else
+                                pmc[1]["hbm_bytes_per_launch"].get(dom)}}
+
+
 def make_fold(P, E, rank):
     from trigenicinteractionpredictor_amd.data import FoldSpec, write_fold
     d = tempfile.mkdtemp(prefix="mmsbm_bench_r%d_" % rank)
@@ -268,8 +335,9 @@ def main():
         else:
             dist.init_process_group(args.backend)
 
-    from trigenicinteractionpredictor_amd import EMEngine, Model
+    from trigenicinteractionpredictor_amd import EMEngine, Model, _lib
     from trigenicinteractionpredictor_amd.layout import links_to_arrays, n_observations
+    build_id = _lib.build_id()
 
     import contextlib
     import io
@@ -281,13 +349,10 @@ def main():
     # restart sharding: global sample s = rank*B + b; one RNG stream seeded once, like :1149/:1260.
     # link sharding: every rank holds the same B samples (s = 0..B-1) and 1/world of the links.
     first = 0 if links_mode else rank * B
-    random.seed(args.seed)
-    thetas, prs = [], []
-    for s in range(first + B):
-        host.initialize_parameters(K)
-        if s >= first:
-            thetas.append(np.array(host._theta))
-            prs.append(np.array(host._pr))
+    from trigenicinteractionpredictor_amd.restarts import (gather_rows, init_samples, replay_check,
+                                                           result_rows, rows_digest)
+    sample_ids = list(range(first, first + B))
+    thetas, prs = init_samples(host, K, sample_ids, args.seed)
     eng = EMEngine(K, host.P, B=B, device=dev)
     ids, counts = host._link_arrays(0)           # the native reader's arrays (links order)
     tids, tcounts = host._link_arrays(1)
@@ -328,39 +393,33 @@ def main():
     # for the roofline; the in-loop events above also time the dependent-launch boundary)
     b2b = {k: eng.time_kernel(k, args.roofline_launches) for k in eng.KERNELS}
     elapsed = t1 - t0
-    L = torch.from_numpy(runner.loglik(0)).to(coll)
+    L = runner.loglik(0)
+    rows = result_rows(sample_ids, L)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        gathered = [torch.empty_like(L) for _ in range(world)]
-        dist.all_gather(gathered, L)       # RCCL gather of final likelihoods
-        L_all = torch.cat(gathered).cpu().numpy()
-    else:
-        L_all = L.cpu().numpy()
-    n_gathered = int(L_all.shape[0])
+        if not links_mode:   # RCCL all-gather of (sample, final L) over xGMI
+            rows = gather_rows(rows, B * world, device=coll)
+    n_gathered = int(rows.shape[0])
+    scale_check = None
+    if rank == 0 and world > 1 and not links_mode:
+        # every sample replayed as ONE batch on this GPU: a sample's bits do not depend on its
+        # batch or rank, so the gathered values must equal the replay bit for bit
+        def factory(nb):
+            e = EMEngine(K, host.P, B=nb, device=dev)
+            e.set_links(0, ids, counts)
+            e.set_links(1, tids, tcounts)
+            return e
+        scale_check = replay_check(rows, host, K, args.seed, args.warmup + args.steps, factory)
 
     if rank == 0:
         iters_total = args.steps * B * (1 if links_mode else world)
         value = iters_total / elapsed
-        work = kernel_work(plan, K, host.P, 2, B, E_obs)
-        dom = max(b2b, key=b2b.get)          # the dominant kernel of the iteration
-        dom_s = b2b[dom] / 1e3
-        fl, by = work[dom]
-        tf, gbs = fl / dom_s / 1e12, by / dom_s / 1e9
-        f_mfma, f_hbm = tf / FP64_PEAK_TFLOPS, gbs / HBM_PEAK_GBS
-        bound = "mfma" if f_mfma >= f_hbm else "hbm"
-        traffic = None
-        pmc = os.path.join(REPO, "profiles", "pmc_r02_K%d.json" % K)
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                rec = json.load(f)
-            if rec.get("E_obs") == E_obs and rec.get("B") == B:
-                traffic = rec.get("hbm_bytes_per_launch", {}).get(dom)
         iter_s = elapsed / args.steps
+        roofline = roofline_record(K, host.P, 2, B, E_obs, plan, iter_s, b2b, build_id)
         wl = ("fold0 stand-in" if (args.P, args.E) == (1500, 90000) else
               "synthetic P=%d, E=%d" % (host.P, args.E))
-        s8d_flops = 8.0 * K ** 3 * E_obs * B      # SURVEY.md 8d's credit for one iteration
         line = {
             "metric": "EM-iterations/sec + final log-likelihood, fold0 K=%d" % K,
             "value": value,
@@ -382,29 +441,14 @@ def main():
                        "parallelism": ("link-sharded x%d" if links_mode else "restart-sharded x%d") % world},
             "world_size": dist.get_world_size() if world > 1 else 1,
             "gathered_samples": n_gathered,
-            "final_loglik": float(L_all[0]),
-            "final_loglik_best": float(L_all.max()),
-            "roofline": {"bound": bound,
-                         "achieved": tf if bound == "mfma" else gbs,
-                         "peak": FP64_PEAK_TFLOPS if bound == "mfma" else HBM_PEAK_GBS,
-                         "unit": "TFLOP/s" if bound == "mfma" else "GB/s",
-                         "frac": f_mfma if bound == "mfma" else f_hbm,
-                         "traffic": traffic,
-                         "kernel": KERNEL_NAMES[dom] % K,
-                         "avg_launch_us": dom_s * 1e6,
-                         "algorithmic_flops_per_launch": fl,
-                         "algorithmic_bytes_per_launch": by,
-                         "mfma": {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "frac": f_mfma},
-                         "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "frac": f_hbm}},
-            "iteration": {"us": iter_s * 1e6,
-                          "s8d_credit_flops": s8d_flops,
-                          "s8d_effective_tflops": s8d_flops / iter_s / 1e12,
-                          # the same credit against the FP64 MFMA peak (SURVEY 8d's binding
-                          # roof for K >= 3): whole iteration, all three kernels
-                          "s8d_frac": s8d_flops / iter_s / 1e12 / FP64_PEAK_TFLOPS,
-                          "note": "SURVEY 8d credits 8 K^3 FLOPs per observation (the reference's "
-                                  "per-link lattice); the pivot-run factorisation executes "
-                                  "O(K^2) per observation + O(K^3) per gene (DESIGN.md)"},
+            "final_loglik": float(rows[0, 1]),
+            "final_loglik_best": float(rows[:, 1].max()),
+            "samples": {"digest": rows_digest(rows),
+                        "rows": rows.tolist() if n_gathered <= 64 else None,
+                        "replay_check": scale_check},
+            "build_id": build_id,
+            "roofline": roofline,
+            "iteration": {"us": iter_s * 1e6},
             "kernel_us": {k: {"back_to_back": b2b[k] * 1e3,
                               "in_loop": in_loop[k][0] * 1e3 / max(in_loop[k][1], 1)}
                           for k in eng.KERNELS},
@@ -414,10 +458,14 @@ def main():
         if cpu_rec is not None:
             line["vs_cpu_baseline"] = value / cpu_rec["value"]
         print(json.dumps(line), flush=True)
+    rc = 0
+    if scale_check is not None and not scale_check["bitwise_equal"]:
+        print("bench.py: gathered per-sample results differ from the one-GPU replay", file=sys.stderr)
+        rc = 3
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

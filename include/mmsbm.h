@@ -52,6 +52,9 @@ typedef struct mmsbm_ctx mmsbm_ctx;
 
 int mmsbm_version(void);
 int mmsbm_chunk(void);
+/* 16 hex digits naming the build (sha256 of the sources, headers, arch and flags): profile
+ * records are stamped with it so a measurement can be matched to the library it came from. */
+const char *mmsbm_build_id(void);
 const char *mmsbm_last_error(void);
 
 /* Context = one GPU + one problem shape.  Replaces the per-process `Model()`
@@ -60,7 +63,9 @@ int mmsbm_create(int device, mmsbm_ctx **out);
 int mmsbm_destroy(mmsbm_ctx *ctx);
 
 /* K groups, R ratings (2 in the reference, :79), B batched samples
- * (independent restarts, :1253), P genes (:413), eps (:88). */
+ * (independent restarts, :1253), P genes (:413), eps (:88).  Changing K, R or P
+ * drops the link sets, the degree and the workspace (call mmsbm_set_links and
+ * mmsbm_set_workspace again); changing B drops the workspace. */
 int mmsbm_set_shape(mmsbm_ctx *ctx, int32_t K, int32_t R, int32_t B, int32_t P, double eps);
 
 /* One link set (MMSBM_SET_TRAIN = `links`, MMSBM_SET_TEST = `test_links`) as the
@@ -75,7 +80,9 @@ int mmsbm_set_links(mmsbm_ctx *ctx, int32_t which, const int32_t *ids_host,
 
 /* deg_host[P]: the degree the M-step divides by (:1016-1018) — for a
  * link-sharded rank the counter over ALL train links, not its own block.  A
- * zero makes mmsbm_iterate / mmsbm_mstep fail with MMSBM_ERR_ZERO_DEGREE. */
+ * zero makes mmsbm_iterate / mmsbm_mstep fail with MMSBM_ERR_ZERO_DEGREE.
+ * The degree is pinned for the NEXT mmsbm_set_links(MMSBM_SET_TRAIN) only: a
+ * train link set given without a preceding mmsbm_set_degree is counted afresh. */
 int mmsbm_set_degree(mmsbm_ctx *ctx, const int32_t *deg_host);
 
 /* Scratch the engine needs (c per observation, partial rows, S partials). */

@@ -315,3 +315,97 @@ def test_context_reshaped_to_another_K_matches_oracle(tmp_path):
         th_o, pr_o = c_oracle.make_iteration(ids, counts, th_o, pr_o)
     np.testing.assert_allclose(th[0], th_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(pr[0], pr_o, rtol=RTOL, atol=ATOL)
+
+
+def test_reshape_without_new_links_is_refused(tmp_path):
+    """mmsbm_set_shape with another K drops the old plans, degree and workspace: iterating before
+    mmsbm_set_links is an error (MMSBM_ERR_INVALID), not a run on the old shape's plan."""
+    from trigenicinteractionpredictor_amd import EMEngine, Model, _lib
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    tr, te = _fold(tmp_path, 300, 5000, seed=22)
+    m = Model()
+    m.get_traintest(tr, te)
+    ids, counts = links_to_arrays(m.links)
+    random.seed(5)
+    m.initialize_parameters(20)
+    eng = EMEngine(20, m.P)
+    eng.set_links(0, ids, counts)
+    eng.upload(np.array(m.theta)[None], np.array(m.pr)[None])
+    eng.iterate(1)
+    for K, B, P in ((10, 1, m.P), (20, 2, m.P), (20, 1, m.P + 7)):
+        _lib.check(eng.lib.mmsbm_set_shape(eng.ctx, 20, 2, 1, m.P, 1e-10))   # back to the start
+        eng.set_links(0, ids, counts)
+        _lib.check(eng.lib.mmsbm_set_shape(eng.ctx, K, 2, B, P, 1e-10))
+        with pytest.raises(_lib.MMSBMError) as err:
+            eng.iterate(1)
+        assert err.value.code == _lib.MMSBM_ERR_INVALID
+        with pytest.raises(_lib.MMSBMError):   # the likelihood call checks its workspace too
+            eng.loglik_async(0)
+    eng.synchronize()
+
+
+def test_degree_override_applies_to_the_next_train_set_only(tmp_path):
+    """mmsbm_set_degree pins the degree for the next train link set; a later set_links(TRAIN)
+    without one counts its own links again (the reference's `counter`, :986-994)."""
+    from oracle import c_oracle
+    from trigenicinteractionpredictor_amd import EMEngine, Model
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    tr, te = _fold(tmp_path, 200, 3000, seed=23)
+    m = Model()
+    m.get_traintest(tr, te)
+    ids, counts = links_to_arrays(m.links)
+    random.seed(6)
+    m.initialize_parameters(4)
+    th0, pr0 = np.array(m.theta), np.array(m.pr)
+    eng = EMEngine(4, m.P)
+    eng.set_links(0, ids, counts, deg=np.full(m.P, 1000, dtype=np.int32))   # a bogus pin
+    eng.set_links(0, ids, counts)                                           # counted afresh
+    eng.upload(th0[None], pr0[None])
+    eng.iterate(1)
+    th, pr = eng.download()
+    th_o, pr_o = c_oracle.make_iteration(ids, counts, th0, pr0)
+    np.testing.assert_allclose(th[0], th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(pr[0], pr_o, rtol=RTOL, atol=ATOL)
+
+
+def test_accumulate_without_train_links_keeps_the_theta_addend(tmp_path):
+    """A context with no train observations: mmsbm_accumulate returns nth = the theta addend
+    (include/mmsbm.h), as the fin path would, and S = 0."""
+    import torch
+    from trigenicinteractionpredictor_amd import EMEngine, _lib
+    P, K = 50, 3
+    eng = EMEngine(K, P)
+    deg = np.ones(P, dtype=np.int32)
+    eng.set_links(0, np.zeros((0, 3), np.int32), np.zeros((0, 2), np.int32), deg=deg)
+    add = torch.rand((1, P, K), dtype=torch.float64, device=eng.device)
+    _lib.check(eng.lib.mmsbm_set_theta_addend(eng.ctx, add.data_ptr()))
+    nth = torch.full((1, P, K), 7.0, dtype=torch.float64, device=eng.device)
+    S = torch.full((1, 2, K ** 3), 7.0, dtype=torch.float64, device=eng.device)
+    eng.accumulate(nth, S)
+    eng.synchronize()
+    assert torch.equal(nth, add)
+    assert torch.count_nonzero(S).item() == 0
+
+
+def test_in_place_link_edit_between_iterations_matches_oracle():
+    """The reference re-reads `links` on every make_iteration (:987): an in-place edit between two
+    iterations (a new rating on one link, a removed link) must reach the device."""
+    from oracle import c_oracle
+    meta, vec, train, test = load("tiny", "K3_s1")
+    m = _gpu_model(train, test)
+    random.seed(meta["seed"])
+    m.initialize_parameters(3)
+    m.make_iteration()
+    th, pr = np.array(m.theta), np.array(m.pr)
+    keys = list(m.links)
+    m.links[keys[0]][1] += 2            # both ratings observed now
+    del m.links[keys[-1]]
+    ids, counts = c_oracle.links_to_arrays(m.links)
+    deg = np.bincount(ids.ravel(), minlength=m.P)
+    assert deg.min() > 0
+    m.make_iteration()
+    th_o, pr_o = c_oracle.make_iteration(ids, counts, th, pr)
+    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(m.compute_likelihood("train"), c_oracle.loglik(ids, counts, th_o, pr_o),
+                               rtol=RTOL)

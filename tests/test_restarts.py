@@ -14,8 +14,9 @@ import torch.multiprocessing as mp
 from oracle.mmsbm_oracle import OracleModel
 from oracle_engine import OracleEngine
 from trigenicinteractionpredictor_amd.model import Model
-from trigenicinteractionpredictor_amd.restarts import (init_samples, run_restarts, run_samples,
-                                                       shard_samples)
+from trigenicinteractionpredictor_amd.restarts import (fixed_run, gather_rows, init_samples,
+                                                       replay_check, result_rows, rows_digest,
+                                                       run_restarts, run_samples, shard_samples)
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tiny")
 TRAIN, TEST = os.path.join(GOLD, "train.dat"), os.path.join(GOLD, "test.dat")
@@ -110,3 +111,42 @@ def test_two_rank_gloo_gather_matches_single_process():
                           engine_factory=lambda B: OracleEngine(m.links, m.test_links))
     want = [(r.sample, r.iterations, r.converged, r.loglik, r.heldout) for r in single]
     assert got[0] == want and got[1] == want
+
+
+def _fixed_worker(rank, world, port, queue):
+    """bench.py's N>1 path on the oracle: this rank's block of samples for a fixed number of
+    iterations, one all-gather of (sample, L), and rank 0's one-batch replay of all of them."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _host()
+    ids = shard_samples(4, world, rank)
+    th, pr = init_samples(m, 2, ids, seed=9)
+    L = fixed_run(OracleEngine(m.links, m.test_links), th, pr, 6, chunks=(1, 2))
+    rows = gather_rows(result_rows(ids, L), 4)
+    check = None
+    if rank == 0:
+        check = replay_check(rows, m, 2, 9, 6, lambda B: OracleEngine(m.links, m.test_links))
+    queue.put((rank, rows_digest(rows), check))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_fixed_run_digest_equals_one_rank_and_replay():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 500) % 1000
+    procs = [ctx.Process(target=_fixed_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {r: (d, c) for r, d, c in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    m = _host()
+    th, pr = init_samples(m, 2, list(range(4)), seed=9)
+    one = rows_digest(result_rows(range(4), fixed_run(OracleEngine(m.links, m.test_links), th, pr, 6)))
+    assert got[0][0] == got[1][0] == one
+    check = got[0][1]
+    assert check["bitwise_equal"] and check["samples"] == 4
+    assert check["digest"] == check["replay_digest"] == one

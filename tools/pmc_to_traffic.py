@@ -1,7 +1,10 @@
-"""profiles/pmc_r02_K<K>.json from a tools/gpu_r02_prof.sh output directory: HBM bytes per launch
-of each kernel of the iteration = 2 x FETCH_SIZE (gfx950: FETCH_SIZE tallies 128-B requests at
-64 B, MI355X_MICROARCH.md) + WRITE_SIZE, both in KiB per dispatch, averaged over the dispatches
-of the PMC passes.  usage: python tools/pmc_to_traffic.py gpurun_out/<tag> K E_obs B out.json"""
+"""profiles/pmc_<round>_K<K>.json from a tools/gpu_r03_prof.sh output directory: HBM bytes per
+launch of each kernel of the iteration = 2 x FETCH_SIZE (gfx950: FETCH_SIZE tallies 128-B requests
+at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE, both in KiB per dispatch, averaged over the dispatches
+of the PMC passes.  The record is stamped with the build id of the library the passes ran (the
+`build_id` field of the bench lines they printed, which must all agree): bench.py only reports a
+record whose build id equals its own library's.
+usage: python tools/pmc_to_traffic.py gpurun_out/<tag> K E_obs B out.json"""
 import collections
 import csv
 import glob
@@ -17,7 +20,15 @@ def main(root, K, E_obs, B, out):
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    rec = {"K": K, "E_obs": E_obs, "B": B, "source": root, "hbm_bytes_per_launch": {}, "counters": {}}
+    ids = set()
+    for f in sorted(glob.glob(root + "/p*.log")):
+        for line in open(f, errors="replace"):
+            if line.startswith("{") and '"build_id"' in line:
+                ids.add(json.loads(line)["build_id"])
+    if len(ids) != 1:
+        sys.exit("pmc_to_traffic: expected one build id in %s/p*.log, found %s" % (root, sorted(ids)))
+    rec = {"K": K, "E_obs": E_obs, "B": B, "source": root, "build_id": ids.pop(),
+           "hbm_bytes_per_launch": {}, "counters": {}}
     for pat, key in NAMES.items():
         cs = acc.get(pat % K)
         if not cs:

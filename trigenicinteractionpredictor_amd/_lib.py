@@ -30,6 +30,7 @@ _c_int, _c_i32, _c_i64, _c_dbl, _vp = ctypes.c_int, ctypes.c_int32, ctypes.c_int
 SIGNATURES = {
     "mmsbm_version": (_c_int, []),
     "mmsbm_chunk": (_c_int, []),
+    "mmsbm_build_id": (ctypes.c_char_p, []),
     "mmsbm_last_error": (ctypes.c_char_p, []),
     "mmsbm_create": (_c_int, [_c_int, ctypes.POINTER(_vp)]),
     "mmsbm_destroy": (_c_int, [_vp]),
@@ -88,6 +89,11 @@ def load(path: str = LIB) -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def build_id() -> str:
+    """The loaded library's build id (include/mmsbm.h, mmsbm_build_id)."""
+    return load().mmsbm_build_id().decode()
 
 
 def check(rc: int) -> None:

@@ -49,8 +49,34 @@ def link_command(out: str, objs) -> list[str]:
 
 def command(out: str = LIB, extra=()) -> list[str]:
     """One-shot build of every source into `out` (measurement builds with extra -D flags)."""
+    bid_src = _write_build_id(os.path.dirname(os.path.abspath(out)), build_id(extra))
     return [hipcc(), "-O3", "-std=c++17", "--offload-arch=" + ARCH, "-fPIC", "-shared",
-            "-I" + INCLUDE, "-o", out, *SRCS, *extra]
+            "-I" + INCLUDE, "-o", out, *SRCS, bid_src, *extra]
+
+
+def build_id(extra=()) -> str:
+    """16 hex digits of sha256 over every source and header the library is built from, the
+    offload arch and the compile flags: names the build a profile record was taken with
+    (bench.py compares it with the loaded library's mmsbm_build_id())."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted({f for src in SRCS for f in [src, *DEPS[src]]})
+    for f in files:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(["-O3", "-std=c++17", "--offload-arch=" + ARCH, *extra]).encode())
+    return h.hexdigest()[:16]
+
+
+def _write_build_id(out_dir: str, bid: str) -> str:
+    """A one-function host source that returns the build id (compiled and linked last)."""
+    src = os.path.join(out_dir, "build_id.cpp")
+    text = 'extern "C" const char* mmsbm_build_id(void) { return "%s"; }\n' % bid
+    if not os.path.exists(src) or open(src).read() != text:
+        with open(src, "w") as f:
+            f.write(text)
+    return src
 
 
 def _stale(target: str, deps) -> bool:
@@ -83,6 +109,10 @@ def build(force: bool = False, verbose: bool = True) -> str:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, "hipcc " + obj)
         os.replace(obj + ".tmp", obj)
+    bid_obj = os.path.join(OUT_DIR, "build_id.o")
+    bid_src = _write_build_id(OUT_DIR, build_id())
+    subprocess.check_call([shutil.which("g++") or "g++", "-O2", "-fPIC", "-c", "-o", bid_obj, bid_src])
+    objs.append(bid_obj)
     tmp = LIB + ".tmp"
     cmd = link_command(tmp, objs)
     if verbose:

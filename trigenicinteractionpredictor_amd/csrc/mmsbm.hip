@@ -1195,7 +1195,7 @@ struct mmsbm_ctx {
   SetDev sets[2];
   int* deg = nullptr;            // device, owned
   std::vector<int> deg_host;
-  bool deg_override = false;     // mmsbm_set_degree: a link-sharded rank's global counter
+  bool deg_pending = false;      // mmsbm_set_degree: the next set_links(TRAIN) keeps this degree
   bool zero_degree = false;
   char* ws = nullptr;
   long long ws_bytes = 0;
@@ -1487,6 +1487,23 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
   if (B < 1 || B > 65535) return fail(MMSBM_ERR_INVALID, "B=%d outside [1, 65535]", B);
   if (P < 1) return fail(MMSBM_ERR_INVALID, "P=%d < 1", P);
   if (!(eps >= 0.0)) return fail(MMSBM_ERR_INVALID, "eps must be >= 0");
+  if (K != c->K || R != c->R || P != c->P) {
+    // the link plans (gene caps, partial-row sizes), the degree and the workspace were built for
+    // the old shape: the caller sets links (and the workspace) again
+    DeviceGuard g(c->device);
+    for (auto& sd : c->sets) sd.release();
+    if (c->deg) (void)hipFree(c->deg);
+    c->deg = nullptr;
+    c->deg_host.clear();
+    c->deg_pending = false;
+    c->zero_degree = false;
+    c->ws = nullptr;
+    c->ws_bytes = 0;
+  }
+  if (B != c->B) {  // the workspace holds B samples' scratch
+    c->ws = nullptr;
+    c->ws_bytes = 0;
+  }
   c->K = K;
   c->R = R;
   c->B = B;
@@ -1560,11 +1577,12 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   ++c->gen;
   c->ws = nullptr;  // the workspace layout changed: mmsbm_set_workspace again
   if (em) {
-    if (!c->deg_override) {
+    if (!c->deg_pending) {  // no mmsbm_set_degree since the last train set: count this one
       std::vector<int> deg(c->P, 0);  // the reference's `counter` (:986-994)
       for (int64_t q = 0; q < E * 3; ++q) deg[ids_host[q]]++;
       if ((rc = set_degree(c, deg))) return rc;
     }
+    c->deg_pending = false;
   }
   return MMSBM_OK;
 }
@@ -1574,7 +1592,7 @@ int mmsbm_set_degree(mmsbm_ctx* c, const int32_t* deg_host) {
   int rc = check_shape(c);
   if (rc) return rc;
   DeviceGuard g(c->device);
-  c->deg_override = true;
+  c->deg_pending = true;
   return set_degree(c, std::vector<int>(deg_host, deg_host + c->P));
 }
 
@@ -1731,7 +1749,11 @@ int mmsbm_accumulate(mmsbm_ctx* c, const double* theta, const double* pr, double
   double* th = const_cast<double*>(theta);  // the passes only read theta / pr; fin in sums mode
   double* p = const_cast<double*>(pr);      // writes nth / S and leaves them untouched
   if (c->sets[MMSBM_SET_TRAIN].h.n_obs == 0) {  // a rank without train links adds zeros
-    HIP_TRY(hipMemsetAsync(nth, 0, sizeof(double) * c->B * c->P * c->K, s));
+    if (c->nth_add)  // the joint model's pair sums still count (fin would add them)
+      HIP_TRY(hipMemcpyAsync(nth, c->nth_add, sizeof(double) * c->B * c->P * c->K,
+                             hipMemcpyDeviceToDevice, s));
+    else
+      HIP_TRY(hipMemsetAsync(nth, 0, sizeof(double) * c->B * c->P * c->K, s));
     HIP_TRY(hipMemsetAsync(S, 0, sizeof(double) * c->B * c->R * c->K * c->K * c->K, s));
     return MMSBM_OK;
   }
@@ -1760,7 +1782,8 @@ int mmsbm_loglik(mmsbm_ctx* c, int32_t which, const double* theta, const double*
   if (rc) return rc;
   if (which != MMSBM_SET_TRAIN && which != MMSBM_SET_TEST)
     return fail(MMSBM_ERR_INVALID, "which=%d", which);
-  if (!c->ws) return fail(MMSBM_ERR_INVALID, "workspace missing");
+  if (!c->ws || c->ws_bytes < (long long)ws_layout(c).total)
+    return fail(MMSBM_ERR_INVALID, "workspace missing or too small (mmsbm_workspace_bytes)");
   if (!theta || !pr || !out) return fail(MMSBM_ERR_INVALID, "null pointer");
   DeviceGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;

@@ -32,6 +32,7 @@ import numpy as np
 
 from . import _lib
 from .layout import links_to_arrays
+from .tracked import TrackedTable, version_of
 
 HO_DELTA = "hoΔ"   # the filler allele removed from every key (:318-323, :405-410)
 
@@ -200,6 +201,10 @@ class Model:
     """`Model` of src/TrigenicInteractionPredictor_23.py (:37-1697) under the spec fix."""
 
     Engine = JointEngine   # device engine class (tests substitute a CPU checker engine)
+    # the train tables the device copy is built from; in-place edits change their version
+    # (tracked.py), as the reference re-reads them on every call (:1572-1617)
+    links = TrackedTable()
+    dlinks = TrackedTable()
 
     def __init__(self, device=None):
         self.nTheta = []
@@ -262,7 +267,7 @@ class Model:
         self._engine_key = None
 
     def _ensure_engine(self):
-        key = (self.K, self.P, id(self.links), len(self.links), id(self.dlinks), len(self.dlinks))
+        key = (self.K, self.P, version_of(self.links), version_of(self.dlinks))
         if self._engine is None or self._engine_key != key:
             if self._engine is not None:
                 self._pull()
@@ -349,7 +354,8 @@ class Model:
     def _add(table, key, r):
         row = table.get(key)
         if row is None:
-            row = table[key] = [0] * 2
+            table[key] = [0] * 2
+            row = table[key]   # a tracked table stores its own row object
         row[r] += 1
 
     @staticmethod

@@ -23,6 +23,7 @@ import numpy as np
 
 from . import _lib
 from .layout import links_to_arrays
+from .tracked import TrackedLinks, version_of
 
 
 NATIVE_INGEST = True   # get_traintest's native reader for canonical files (ingest.py)
@@ -32,7 +33,7 @@ class Model:
     def __init__(self, device=None):
         self._links_version = 0
         self._fold = None               # native parse backing the lazy link dicts (ingest.py)
-        self._fold_fresh = [False, False]
+        self._fold_v = [None, None]     # table version that still equals the parsed arrays
         self.ntheta = []
         self._theta = []
         self.id_gene = {}
@@ -92,36 +93,34 @@ class Model:
 
     # ---------------------------------------------- link tables (lazy after a native parse)
     # After get_traintest's native reader, `links` / `nlinks` / `test_links` are built as the
-    # reference's dicts on first access; until a caller has touched them the engine and the
-    # counts below read the parsed arrays directly.  The device copy of a link table is made
-    # when the engine is built: assigning a new table (the setters) or calling
-    # `links_changed()` after editing a dict in place makes the next call rebuild it (the
-    # reference re-reads the dicts on every call, :987, :959).
+    # reference's dicts on first access; until then the engine reads the parsed arrays.  The
+    # tables are TrackedLinks (tracked.py): every in-place edit (`links[k][r] += 1`,
+    # `links[k] = [..]`, `del links[k]`, ...) changes their version, and so does assigning a new
+    # table.  The device copy is rebuilt whenever the versions differ from the ones it was built
+    # from, as the reference re-reads the dicts on every call (:987, :959).
     @property
     def links(self):
         if self._links is None:
-            self._links = self._fold.links_dict()
-        self._fold_fresh[0] = False     # the caller may edit the dict
+            self._links = TrackedLinks(self._fold.links_dict())
+            self._fold_v[0] = self._links.version.n
         return self._links
 
     @links.setter
     def links(self, value):
-        self._links = value
-        self._fold_fresh[0] = False
-        self._links_version += 1        # a new table: the engine re-reads it
+        self._links = value if isinstance(value, TrackedLinks) else TrackedLinks(value)
+        self._fold_v[0] = None
 
     @property
     def test_links(self):
         if self._test_links is None:
-            self._test_links = self._fold.test_links_dict()
-        self._fold_fresh[1] = False
+            self._test_links = TrackedLinks(self._fold.test_links_dict())
+            self._fold_v[1] = self._test_links.version.n
         return self._test_links
 
     @test_links.setter
     def test_links(self, value):
-        self._test_links = value
-        self._fold_fresh[1] = False
-        self._links_version += 1
+        self._test_links = value if isinstance(value, TrackedLinks) else TrackedLinks(value)
+        self._fold_v[1] = None
 
     @property
     def nlinks(self):
@@ -134,24 +133,32 @@ class Model:
         self._nlinks = value
 
     def links_changed(self):
-        """Declare an in-place edit of `links` / `test_links`: the device tables are rebuilt."""
+        """Declare an edit the tables cannot see (e.g. of a dict object kept from before it was
+        assigned to `links`): the device tables are rebuilt on the next call."""
         self._links_version += 1
+
+    def _fold_fresh(self, which):
+        """The parsed arrays still hold table `which` (nothing edited or replaced it)."""
+        if self._fold is None or self._fold_v[which] is None:
+            return False
+        tab = self._links if which == 0 else self._test_links
+        return tab is None or tab.version.n == self._fold_v[which]
 
     def _link_arrays(self, which):
         """(ids int32[E][3] in key order, counts int32[E][R]) of the train (0) / test (1) links."""
-        if self._fold is not None and self._fold_fresh[which]:
+        if self._fold_fresh(which):
             f = self._fold
             return (f.train_ids, f.train_counts) if which == 0 else (f.test_ids, f.test_counts)
         return links_to_arrays(self.links if which == 0 else self.test_links, self.R)
 
     def _n_links(self, which=0):
-        if self._fold is not None and self._fold_fresh[which]:
+        if self._fold_fresh(which):
             return int((self._fold.train_ids if which == 0 else self._fold.test_ids).shape[0])
         return len(self.links if which == 0 else self.test_links)
 
     def _ensure_engine(self):
         from .engine import EMEngine  # imports torch + the HIP library
-        key = (self.K, self.P, self._links_version)
+        key = (self.K, self.P, self._links_version, version_of(self._links), version_of(self._test_links))
         if self._engine is None or self._engine_key != key:
             if self._engine is not None:
                 self._pull()
@@ -227,7 +234,8 @@ class Model:
     def _add(self, table, key, r):
         row = table.get(key)
         if row is None:
-            row = table[key] = [0] * 2
+            table[key] = [0] * 2
+            row = table[key]   # a tracked table stores its own row object
         row[r] += 1
 
     def get_input(self, argfilename, selectedinteractiontype="trigenic", cutoffvalue=-0.08, discard=0,
@@ -283,7 +291,7 @@ class Model:
             self.gene_id = {g: i for i, g in enumerate(fold.names)}
             self.uniqueg = dict(enumerate(fold.uniqueg.tolist()))
             self._links = self._nlinks = self._test_links = None
-            self._fold_fresh = [True, True]
+            self._fold_v = [0, 0]
             self.P = fold.P
             self._links_version += 1
             n_train = self._n_links(0)
@@ -395,7 +403,7 @@ class Model:
         self.results.reverse()
 
     def calculate_metrics(self):
-        if self._fold is not None and self._fold_fresh[0]:
+        if self._fold_fresh(0):
             positives = int((self._fold.train_counts[:, 1] == 1).sum())
         else:
             positives = sum(1 for n in self.links.values() if n[1] == 1)

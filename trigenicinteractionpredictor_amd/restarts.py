@@ -154,3 +154,66 @@ def run_restarts(model, K, n_samples, seed, iterations=10000, fcheck=25, bcheck=
     if not dist_on:
         return local
     return gather_results(local, n_samples, group=group, device=device)
+
+
+# ------------------------------------------------------------------ fixed-length runs (bench.py)
+# bench.py runs every rank's block of samples for a fixed number of iterations (no convergence
+# stop), gathers (sample id, final train log-likelihood) from every rank and, on rank 0, replays
+# all samples as ONE batch on one engine: a sample's bits do not depend on its batch or its rank
+# (DESIGN.md), so the gathered values must equal the replay bit for bit.  The digest names the
+# per-sample results of a run, so runs at different GPU counts can be compared.
+
+def fixed_run(engine, thetas, prs, iterations: int, chunks=()):
+    """Upload, run `iterations` EM iterations (in the given chunk sizes when they are given),
+    and return the final train log-likelihood of every sample."""
+    engine.upload(np.stack(thetas), np.stack(prs))
+    done = 0
+    for n in chunks:
+        engine.iterate(n)
+        done += n
+    if iterations > done:
+        engine.iterate(iterations - done)
+    return np.array(engine.loglik(TRAIN), dtype=np.float64)
+
+
+def result_rows(sample_ids, loglik) -> np.ndarray:
+    """[n][2] float64 rows (sample id, final log-likelihood)."""
+    return np.stack([np.asarray(sample_ids, dtype=np.float64),
+                     np.asarray(loglik, dtype=np.float64)], axis=1).reshape(-1, 2)
+
+
+def gather_rows(rows: np.ndarray, n_samples: int, group=None, device=None) -> np.ndarray:
+    """All-gather every rank's rows (one collective: RCCL all-gather over xGMI under nccl),
+    sorted by sample id."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    width = -(-n_samples // world)
+    buf = torch.full((width, 2), float("nan"), dtype=torch.float64)
+    buf[:rows.shape[0]] = torch.from_numpy(np.ascontiguousarray(rows))
+    if device is not None:
+        buf = buf.to(device)
+    out = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf, group=group)
+    got = torch.cat(out).cpu().numpy()
+    got = got[~np.isnan(got[:, 0])]
+    return got[np.argsort(got[:, 0], kind="stable")]
+
+
+def rows_digest(rows: np.ndarray) -> str:
+    """sha256 (16 hex digits) of the rows sorted by sample id, as float64 bytes."""
+    import hashlib
+    r = np.ascontiguousarray(rows[np.argsort(rows[:, 0], kind="stable")], dtype=np.float64)
+    return hashlib.sha256(r.tobytes()).hexdigest()[:16]
+
+
+def replay_check(rows: np.ndarray, model, K: int, seed: int, iterations: int, engine_factory,
+                 chunks=()) -> dict:
+    """Replay every gathered sample as one batch (engine_factory(B)) from the same RNG stream and
+    compare bit for bit.  -> {"samples", "digest", "replay_digest", "bitwise_equal"}."""
+    ids = [int(s) for s in rows[:, 0]]
+    thetas, prs = init_samples(model, K, ids, seed)
+    L = fixed_run(engine_factory(len(ids)), thetas, prs, iterations, chunks)
+    rep = result_rows(ids, L)
+    return {"samples": len(ids), "digest": rows_digest(rows), "replay_digest": rows_digest(rep),
+            "bitwise_equal": bool(np.array_equal(rows[:, 1].view(np.int64), rep[:, 1].view(np.int64)))}

@@ -1,0 +1,178 @@
+"""Link tables that notice in-place edits.
+
+The reference re-reads `self.links` / `self.test_links` on every call
+(src/TrigenicInteractionPredictor.py:987 in make_iteration, :959 in
+compute_likelihood), so a caller may edit them between iterations:
+`model.links[key][1] += 1`, `model.links[key] = [0, 1]`, `del model.links[key]`.
+The engine keeps a device copy of each table (its work plan), so it must learn of
+such edits.  `TrackedLinks` is a dict whose values are `TrackedRow` lists; every
+mutating method of either bumps one shared counter, which the Model compares before
+each device call (an O(1) check, no re-scan of the table).
+
+Both types are plain dict / list subclasses: iteration order, equality, `json`,
+`copy` and `isinstance(x, dict)` behave as for the reference's objects.
+"""
+from __future__ import annotations
+
+import itertools
+
+_clock = itertools.count(1)   # one clock for every table: a number is never reused
+
+
+class Version:
+    """`n` changes at every edit and differs between tables, so a tuple of the `n` of the tables
+    a device copy was built from identifies exactly that state."""
+    __slots__ = ("n",)
+
+    def __init__(self):
+        self.n = next(_clock)
+
+    def bump(self):
+        self.n = next(_clock)
+
+
+class TrackedRow(list):
+    """The rating counts [n_0, n_1, ...] of one link; edits bump the owner's counter."""
+    __slots__ = ("_v",)
+
+    def __init__(self, it=(), version: Version = None):
+        super().__init__(it)
+        self._v = version
+
+    def _bump(self):
+        if self._v is not None:
+            self._v.bump()
+
+    def __setitem__(self, i, x):
+        super().__setitem__(i, x)
+        self._bump()
+
+    def __delitem__(self, i):
+        super().__delitem__(i)
+        self._bump()
+
+    def __iadd__(self, other):
+        r = super().__iadd__(other)
+        self._bump()
+        return r
+
+    def __imul__(self, n):
+        r = super().__imul__(n)
+        self._bump()
+        return r
+
+    def append(self, x):
+        super().append(x)
+        self._bump()
+
+    def extend(self, it):
+        super().extend(it)
+        self._bump()
+
+    def insert(self, i, x):
+        super().insert(i, x)
+        self._bump()
+
+    def pop(self, *a):
+        r = super().pop(*a)
+        self._bump()
+        return r
+
+    def remove(self, x):
+        super().remove(x)
+        self._bump()
+
+    def reverse(self):
+        super().reverse()
+        self._bump()
+
+    def sort(self, *a, **kw):
+        super().sort(*a, **kw)
+        self._bump()
+
+    def clear(self):
+        super().clear()
+        self._bump()
+
+    def __reduce_ex__(self, protocol):   # pickles / deep-copies as a plain list
+        return (list, (list(self),))
+
+
+class TrackedLinks(dict):
+    """`links` / `test_links`: key 'i_j_k' -> TrackedRow of counts.  Any edit of the table or of
+    one of its rows bumps `version.n`."""
+
+    def __init__(self, src=None, version: Version = None):
+        super().__init__()
+        self.version = version if version is not None else Version()
+        if src:
+            for k, v in (src.items() if hasattr(src, "items") else src):
+                dict.__setitem__(self, k, self._row(v))
+
+    def _row(self, v):
+        if isinstance(v, list):
+            if isinstance(v, TrackedRow) and v._v is self.version:
+                return v
+            return TrackedRow(v, self.version)
+        return v
+
+    def __setitem__(self, k, v):
+        dict.__setitem__(self, k, self._row(v))
+        self.version.bump()
+
+    def __delitem__(self, k):
+        dict.__delitem__(self, k)
+        self.version.bump()
+
+    def setdefault(self, k, default=None):
+        if k in self:
+            return dict.__getitem__(self, k)
+        self[k] = default
+        return dict.__getitem__(self, k)
+
+    def update(self, *a, **kw):
+        for k, v in dict(*a, **kw).items():
+            dict.__setitem__(self, k, self._row(v))
+        self.version.bump()
+
+    def __ior__(self, other):
+        self.update(other)
+        return self
+
+    def pop(self, *a):
+        r = dict.pop(self, *a)
+        self.version.bump()
+        return r
+
+    def popitem(self):
+        r = dict.popitem(self)
+        self.version.bump()
+        return r
+
+    def clear(self):
+        dict.clear(self)
+        self.version.bump()
+
+    def __reduce_ex__(self, protocol):   # pickles / deep-copies as a plain dict of lists
+        return (dict, ({k: list(v) if isinstance(v, list) else v for k, v in self.items()},))
+
+
+def version_of(table) -> int:
+    """The state number of a tracked table (0 for None: not materialised yet)."""
+    return 0 if table is None else table.version.n
+
+
+class TrackedTable:
+    """Class attribute that keeps a TrackedLinks in the instance: assigning a plain dict stores a
+    tracked copy of it (a new table, with a new version)."""
+
+    def __set_name__(self, owner, name):
+        self.slot = "_tracked_" + name
+
+    def __get__(self, obj, owner=None):
+        if obj is None:
+            return self
+        return obj.__dict__[self.slot]
+
+    def __set__(self, obj, value):
+        obj.__dict__[self.slot] = value if isinstance(value, TrackedLinks) else TrackedLinks(value)
