@@ -120,6 +120,18 @@ def kernel_work(plan, K, P, R, B, E_obs):
     prow0 = plan["partial_rows_stream0"]
     genes_a = plan["v_genes"]
     params = 8.0 * (P * K + R * K3)
+    if plan.get("small_k"):
+        # small-K kernels (csrc/sk.h): per stream-0 stretch a V table, an X contraction and an S
+        # update (2K^3 each); per stream-1/2 stretch an X contraction; bytes: records, row12 and
+        # the c scatter, X partials (K per partial row), S partials (K^3 per stream-0 workgroup)
+        wga = plan["wg_stream0"]
+        a_fl = E_obs * (4.0 * K2 + 2.0 * K) + prow0 * 3 * 2.0 * K3
+        a_by = 24.0 * rows0 + 16.0 * E_obs + 8.0 * K * prow0 + 8.0 * K3 * wga + params
+        b_fl = E_obs * 4.0 * K2 + (prows - prow0) * 2.0 * K3
+        b_by = 24.0 * (rows - rows0) + 8.0 * K * (prows - prow0) + params
+        f_fl = 1.0 * prows * K + R * K3 * wga + 3.0 * P * K + 3.0 * R * K3
+        f_by = 8.0 * K * prows + 8.0 * K3 * wga + 2 * params + 4.0 * 6 * P
+        return {"pass_a": (a_fl * B, a_by * B), "pass_b": (b_fl * B, b_by * B), "fin": (f_fl * B, f_by * B)}
     a_fl = E_obs * (4.0 * K2 + 2.0 * K) + genes_a * 2.0 * K3
     a_by = 16.0 * rows0 + 8.0 * rows0 + 8.0 * K2 * prow0 + params
     b_fl = E_obs * 4.0 * K2 + prow0 * 2.0 * K3

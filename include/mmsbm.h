@@ -123,9 +123,10 @@ int mmsbm_mstep(mmsbm_ctx *ctx, double *theta, double *pr, const double *nth, co
  * mmsbm_accumulate.  The pointer is read at every launch; it stays set until replaced. */
 int mmsbm_set_theta_addend(mmsbm_ctx *ctx, const double *nth_add);
 
-/* Measurement: info[10] = observations, plan rows (3 streams), stream-0 rows, stream-0
- * workgroups, stream-1/2 workgroups, S-partial workgroups, partial rows, most genes per
- * stream-0 workgroup, V genes over all stream-0 workgroups, stream-0 partial rows. */
+/* Measurement: info[12] = observations, plan rows (3 streams), stream-0 rows, stream-0
+ * workgroups, stream-1/2 workgroups, S partials, partial rows, most genes per stream-0
+ * workgroup (per unit for the small-K plan), V tables computed per iteration, stream-0 partial
+ * rows, 1 if the plan is the small-K one (K <= 12, sk.h), units (waves of work). */
 int mmsbm_plan_info(const mmsbm_ctx *ctx, int32_t which, int64_t *info);
 
 /* Kernel timing for measurement (bench.py): with stride n > 0, mmsbm_iterate records a HIP

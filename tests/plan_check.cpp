@@ -20,6 +20,118 @@ static int fail(const char* what, long long a = 0, long long b = 0) {
   return 1;
 }
 
+// Small-K plan: units of at most GU stretches and LCAP_SK chunks covering every chunk once, their
+// descriptors (stretch starts, pivot genes, partial rows), workgroup unit ranges of one
+// (stream, rating), the c scatter map row12, and the S-partial workgroup ranges.
+static int check_small(const Plan& pl, int R, int P, long long nch) {
+  if ((long long)pl.udesc.size() != pl.n_units * UD) return fail("udesc size");
+  const int n_wg = pl.n_wg_a + pl.n_wg_b;
+  if ((int)pl.wg_ustart.size() != n_wg + 1 || pl.wg_ustart[0] != 0 || pl.wg_ustart[n_wg] != pl.n_units)
+    return fail("wg_ustart");
+  std::vector<int> covered(nch, 0);
+  for (int w = 0; w < n_wg; ++w) {
+    const int s = pl.wg_code[w] >> 4, r = pl.wg_code[w] & 15;
+    if ((w < pl.n_wg_a) != (s == 0)) return fail("stream order", w, s);
+    const int rounds = s == 0 ? pl.rounds_a : pl.rounds_b;
+    if (pl.wg_ustart[w + 1] - pl.wg_ustart[w] > NW * rounds || pl.wg_ustart[w + 1] <= pl.wg_ustart[w])
+      return fail("wg units", w, pl.wg_ustart[w + 1] - pl.wg_ustart[w]);
+    for (int u = pl.wg_ustart[w]; u < pl.wg_ustart[w + 1]; ++u) {
+      const int* d = &pl.udesc[(size_t)u * UD];
+      if (d[14] != pl.wg_code[w]) return fail("unit code", u, d[14]);
+      const int nst = d[5], c0 = d[0], c1 = d[4];
+      if (nst < 1 || nst > GU) return fail("stretches", u, nst);
+      if (c1 - c0 > LCAP_SK || c1 <= c0) return fail("unit length", u, c1 - c0);
+      for (int t = 0; t < GU; ++t) {
+        const int a = d[t], b = t + 1 < nst ? d[t + 1] : c1;
+        if (t >= nst) {
+          if (a != c1) return fail("empty stretch start", u, t);
+          continue;
+        }
+        if (b <= a) return fail("stretch order", u, t);
+        const int q = d[6 + t], g = d[10 + t];
+        if (q < 0 || q >= pl.n_prows || pl.prow_gene[q] != g) return fail("stretch prow", u, t);
+        if (t > 0 && d[10 + t - 1] == g) return fail("stretch not maximal", u, t);
+        for (int c = a; c < b; ++c) {
+          covered[c]++;
+          if (pl.chunk_prow[c] != q) return fail("chunk prow", c, q);
+          for (int k = 0; k < CH; ++k) {
+            const I4& x = pl.rows[(long long)c * CH + k];
+            if ((s == 0 ? x.x : s == 1 ? x.y : x.z) != g) return fail("stretch gene", c, k);
+          }
+        }
+      }
+    }
+    (void)r;
+  }
+  for (long long c = 0; c < nch; ++c)
+    if (covered[c] != 1) return fail("chunk coverage", c, covered[c]);
+  // row12: the stream-1 / stream-2 rows of each real stream-0 row hold the same triple and point
+  // back at it; padding rows map to -1
+  if ((long long)pl.row12.size() != 2 * pl.n_rows0) return fail("row12 size");
+  for (long long q = 0; q < pl.n_rows0; ++q) {
+    const I4& x = pl.rows[q];
+    for (int k = 0; k < 2; ++k) {
+      const int t = pl.row12[2 * q + k];
+      if (x.w <= 0) {
+        if (t != -1) return fail("row12 padding", q, t);
+        continue;
+      }
+      if (t < 0 || pl.n_rows0 + t >= (long long)pl.rows.size()) return fail("row12 range", q, t);
+      const I4& y = pl.rows[pl.n_rows0 + t];
+      if (y.x != x.x || y.y != x.y || y.z != x.z || y.w != q) return fail("row12 target", q, t);
+    }
+  }
+  for (int r = 0; r < R; ++r)
+    for (int w = 0; w < pl.n_wg_a; ++w)
+      if (((pl.wg_code[w] & 15) == r) != (w >= pl.sp_lo[r] && w < pl.sp_hi[r])) return fail("sp range", r, w);
+  // slots: every unit once, in its workgroup's slot range, records copied slot-major; the slot-major
+  // row12 points at the pass-B slot row holding the same observation
+  long long units_seen = 0;
+  for (int g = 0; g < 2; ++g) {
+    const int L = pl.sk_L[g];
+    const int w0 = g == 0 ? 0 : pl.n_wg_a, w1 = g == 0 ? pl.n_wg_a : n_wg;
+    const int per = NW * (g == 0 ? pl.rounds_a : pl.rounds_b);
+    if (pl.sk_slots[g] != (long long)(w1 - w0) * per) return fail("slots", g, pl.sk_slots[g]);
+    for (long long slot = 0; slot < pl.sk_slots[g]; ++slot) {
+      const int* d = &pl.sk_udesc[g][(size_t)slot * UD];
+      const int w = w0 + (int)(slot / per);
+      if (d[14] != pl.wg_code[w]) return fail("slot code", slot, d[14]);
+      if (d[5] == 0) continue;
+      ++units_seen;
+      const int u = pl.wg_ustart[w] + (int)(slot % per);
+      const int* du = &pl.udesc[(size_t)u * UD];
+      if (d[4] != du[4] - du[0] || d[4] > L || d[0] != 0) return fail("slot extent", slot, d[4]);
+      for (int i = 0; i < 4 * d[4]; ++i) {
+        const I4& a = pl.sk_urec[g][(size_t)slot * 4 * L + i];
+        const I4& b = pl.rows[4LL * du[0] + i];
+        if (a.x != b.x || a.y != b.y || a.z != b.z || a.w != b.w) return fail("slot record", slot, i);
+      }
+    }
+  }
+  if (units_seen != pl.n_units) return fail("slot units", units_seen, pl.n_units);
+  {
+    const int La = pl.sk_L[0], Lb = pl.sk_L[1];
+    for (long long i = 0; i < pl.sk_slots[0] * 4 * La; ++i) {
+      const I4& a = pl.sk_urec[0][i];
+      for (int k = 0; k < 2; ++k) {
+        const int t = pl.sk_urow12[2 * i + k];
+        if (t < 0) continue;
+        if (t >= pl.sk_slots[1] * 4 * Lb) return fail("urow12 range", i, t);
+        const I4& b = pl.sk_urec[1][t];
+        if (a.x != b.x || a.y != b.y || a.z != b.z || a.w <= 0) return fail("urow12 target", i, t);
+      }
+    }
+  }
+  for (int sec = 0; sec < 3 * R; ++sec) {
+    const int lo = sec == 0 ? 0 : pl.sk_wg_end[sec - 1], hi = pl.sk_wg_end[sec];
+    for (int w = lo; w < hi; ++w)
+      if (((pl.wg_code[w] >> 4) * R + (pl.wg_code[w] & 15)) != sec) return fail("section", sec, w);
+  }
+  (void)P;
+  printf("ok %zu %lld %d %lld %d\n", pl.rows.size(), pl.n_units, n_wg, pl.n_prows, pl.n_sp);
+  return 0;
+}
+
 int main() {
   long long E;
   int R, P, ua, ub, gcap, sp_rows;
@@ -31,7 +143,9 @@ int main() {
     for (int r = 0; r < R; ++r)
       if (scanf("%d", &counts[e * R + r]) != 1) return fail("counts");
   }
-  const Plan pl = build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows);
+  const bool small = gcap == 0;  // gcap 0: the small-K plan of sk.h (sp_rows = its wg_target)
+  const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows)
+                        : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows);
 
   // 1. every observation appears once per stream, with its count on stream 0 and its stream-0
   //    row on streams 1 / 2; padding rows carry a zero count / the zero c slot
@@ -64,6 +178,8 @@ int main() {
       if (y.x != x.x || y.y != x.y || y.z != x.z || y.w <= 0) return fail("c row mismatch", q, x.w);
     }
   }
+
+  if (small) return check_small(pl, R, P, nch);
 
   // 2. a chunk has one pivot gene; pivots ascend inside each (stream, rating) section
   // 3. workgroups: NW + 1 nondecreasing unit bounds, units at most 64 chunks, stream-0

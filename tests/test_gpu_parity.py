@@ -409,3 +409,26 @@ def test_in_place_link_edit_between_iterations_matches_oracle():
     np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(m.compute_likelihood("train"), c_oracle.loglik(ids, counts, th_o, pr_o),
                                rtol=RTOL)
+
+
+@pytest.mark.parametrize("K,env", [(10, {}), (10, {"MMSBM_SK": "0"}), (12, {"MMSBM_SK_WG": "3"}),
+                                   (7, {"MMSBM_SK_WG": "1", "MMSBM_UNITS": "5,9"}), (13, {})])
+def test_kernel_family_and_unit_rounds_match_oracle(tmp_path, monkeypatch, K, env):
+    """K <= 12 runs the small-K kernels (csrc/sk.h), K > 12 the large-K ones; MMSBM_SK=0 forces the
+    large-K family at K=10 and MMSBM_SK_WG forces several unit rounds per workgroup.  Every variant
+    matches the C oracle (2 iterations, train and held-out likelihood)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tr, te = _fold(tmp_path, 400, 12000, seed=31 + K, multi_frac=0.1, both_frac=0.03)
+    m = _gpu_model(tr, te)
+    random.seed(K)
+    m.initialize_parameters(K)
+    theta0, pr0 = np.array(m.theta), np.array(m.pr)
+    m.make_iterations(2)
+    info = m._engine.plan_info()
+    assert info["small_k"] == (1 if K <= 12 and env.get("MMSBM_SK") != "0" else 0)
+    th_o, pr_o, L_o, LT_o = _oracle_run(m, theta0, pr0, 2)
+    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
+    np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)

@@ -50,6 +50,11 @@ def _links(P, E, seed, R=2, hub=0.0, multi=0.05, both=0.03):
     (300, 5000, (1536, 3072), 33, 16, 30.0),   # hub genes, default unit counts
     (120, 4000, (64, 64), 13, 120, 10.0),  # large-K shape: 13 genes, 120 rows per S partial
     (30, 1500, (1536, 3072), 8, 40, 0.0),  # more units than chunks
+    # small-K plans (gcap 0; sp_rows = the workgroup target): stretch-capped units, descriptors
+    (300, 5000, (1536, 3072), 0, 1024, 30.0),  # hub genes
+    (40, 600, (1, 1), 0, 1024, 0.0),           # one unit per stream: runs split at 32 chunks
+    (200, 6000, (64, 64), 0, 3, 5.0),          # several unit rounds per workgroup
+    (30, 1500, (1536, 3072), 0, 1024, 0.0),    # more units than chunks
 ])
 def test_plan_invariants(plan_check, P, E, units, gcap, sp_rows, hub):
     links = _links(P, E, seed=P + E, hub=hub)

@@ -33,6 +33,21 @@ def main(path):
         if name == "fin":
             print("  ->sync %s" % q(t[:, 4] - t[:, 0]))
             print("  ->rows %s" % q(t[:, 5] - t[:, 0]))
+        if name in ("passA", "passB", "passLL") and (t[:, 7] != 0).all():
+            # small-K kernels (csrc/sk.h): 6 = p staged, 1 = unit prologue done, 2 = chunk loop
+            # done, 3 = unit epilogue done, 7 = kernel end (S reduction / likelihood sum)
+            print("  ->p    %s" % q(t[:, 6] - t[:, 0]))
+            print("  unit prologue %s" % q(t[:, 1] - t[:, 6]))
+            print("  chunk loop    %s" % q(t[:, 2] - t[:, 1]))
+            print("  epilogue      %s" % q(t[:, 3] - t[:, 2]))
+            print("  tail          %s" % q(t[:, 7] - t[:, 3]))
+            print("  wave end      %s" % q(t[:, 7] - t0))
+            ch = t[:, 5]
+            print("  chunks %s  stretches %s" % (q(ch), q(t[:, 4])))
+            if ch.max() > 0 and ch.min() < ch.max():
+                a = np.polyfit(ch, ph2, 1)
+                print("  chunk loop ~ %.0f cycles/chunk + %.0f" % (a[0], a[1]))
+            continue
         if name in ("passA", "passB", "passLL"):
             ch = t[:, 5]
             print("  chunks %s" % q(ch))

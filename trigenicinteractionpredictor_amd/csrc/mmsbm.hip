@@ -1150,6 +1150,8 @@ __global__ __launch_bounds__(256) void predict_kernel(const int* __restrict__ id
   out[(size_t)b * n + row] = dsum;
 }
 
+#include "sk.h"  // the small-K (K <= 12) kernel family
+
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
@@ -1166,8 +1168,12 @@ struct SetDev {  // device copy of one link set's plan
   int* prow_ptr = nullptr;
   int* prow_gene = nullptr;
   int* sp_desc = nullptr;
+  int* sku[2] = {nullptr, nullptr};     // small-K plans (sk.h): slot descriptors of each group,
+  int4* skr[2] = {nullptr, nullptr};    // slot-major records,
+  int* skrow12 = nullptr;               // slot-major row12 of group 0
   void release() {
-    void* ps[] = {rows, chunk_prow, chunk_vslot, wg_units, wg_code, wg_gene, vgenes, prow_ptr, prow_gene, sp_desc};
+    void* ps[] = {rows, chunk_prow, chunk_vslot, wg_units, wg_code, wg_gene, vgenes, prow_ptr, prow_gene, sp_desc,
+                  sku[0], sku[1], skr[0], skr[1], skrow12};
     for (void* p : ps)
       if (p) (void)hipFree(p);
     *this = SetDev();
@@ -1176,12 +1182,17 @@ struct SetDev {  // device copy of one link set's plan
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
+using PassFn = int (*)(mmsbm_ctx*, int mode, int which, const double*, const double*, hipStream_t);
+using FinFn = int (*)(mmsbm_ctx*, bool sums, double*, double*, double*, double*, hipStream_t);
+
 struct Launch {
-  int (*pass)(mmsbm_ctx*, int mode, int which, const double*, const double*, hipStream_t);
-  int (*fin)(mmsbm_ctx*, bool sums, double*, double*, double*, double*, hipStream_t);
+  PassFn pass;
+  FinFn fin;
   int (*mapply)(mmsbm_ctx*, double*, double*, const double*, const double*, hipStream_t);
   int (*predict)(mmsbm_ctx*, const int*, long long, const double*, const double*, double*, hipStream_t);
   int gmax;
+  PassFn sk_pass;  // small-K kernels (sk.h), K <= 12; nullptr above
+  FinFn sk_fin;
 };
 
 }  // namespace
@@ -1192,6 +1203,7 @@ struct mmsbm_ctx {
   int K = 0, R = 0, B = 0, P = 0;
   double eps = 1e-10;
   int gcap = 0;                  // most pivot genes per stream-0 workgroup (<= KT<K>::GMAX)
+  bool sk = false;               // K <= 12: the small-K kernels of sk.h (MMSBM_SK=0: the large-K ones)
   SetDev sets[2];
   int* deg = nullptr;            // device, owned
   std::vector<int> deg_host;
@@ -1235,6 +1247,25 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   const auto& te = c->sets[MMSBM_SET_TEST].h;
   const size_t K2 = (size_t)c->K * c->K, K3 = K2 * c->K, B = c->B;
   size_t off = 0;
+  if (c->sk) {
+    // small-K: c at the stream-1/2 rows, X partials (K per partial row), S partials (K^3 per
+    // stream-0 workgroup), likelihood partials, fin's sums-out scratch
+    L.cbuf = off;
+    off += align_up(B * std::max<long long>(tr.sk_slots[1] * 4 * tr.sk_L[1], 1) * 8);
+    L.prows = off;
+    off += align_up(B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
+    L.spart = off;
+    off += align_up(B * std::max(tr.n_wg_a, 1) * K3 * 8);
+    L.pold = off;
+    L.partL = off;
+    off += align_up(B * std::max({tr.n_wg_a, te.n_wg_a, 1}) * 8);
+    L.nth = off;
+    off += align_up(B * (size_t)c->P * c->K * 8);
+    L.S = off;
+    off += align_up(B * c->R * K3 * 8);
+    L.total = off;
+    return L;
+  }
   L.cbuf = off;
   off += align_up(B * (tr.n_rows0 + 1) * 8);
   L.prows = off;
@@ -1365,14 +1396,91 @@ int launch_predict(mmsbm_ctx* c, const int* ids, long long n, const double* thet
   return MMSBM_OK;
 }
 
+template <int K>
+int launch_sk_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const double* pr,
+                   hipStream_t s) {
+  using T = SKT<K>;
+  const SetDev& sd = c->sets[which];
+  const auto& h = sd.h;
+  const auto& tr = c->sets[MMSBM_SET_TRAIN].h;
+  const long long n_cb = std::max<long long>(tr.sk_slots[1] * 4 * tr.sk_L[1], 1);  // pass B's c layout
+  SkSec sec{};
+  for (int i = 0; i < 3 * MAX_R; ++i) sec.wg_end[i] = h.sk_wg_end[i];
+  const int2* r12 = reinterpret_cast<const int2*>(sd.skrow12);
+  int rc;
+  if (mode == PASS_B) {
+    if (h.n_wg_b == 0) return MMSBM_OK;
+    if ((rc = lds_opt_in(c, 5, &sk_pass_kernel<K, SK_B>, T::LDS))) return rc;
+    sk_pass_kernel<K, SK_B><<<dim3(h.n_wg_b, c->B), NT, T::LDS, s>>>(
+        sd.skr[1], sd.sku[1], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, h.n_wg_a,
+        h.sk_L[1], h.rounds_b, c->P, c->R, n_cb, h.n_prows, h.n_wg_b, c->eps);
+  } else if (mode == PASS_A) {
+    if (h.n_wg_a == 0) return MMSBM_OK;
+    if ((rc = lds_opt_in(c, 4, &sk_pass_kernel<K, SK_A>, T::LDS))) return rc;
+    sk_pass_kernel<K, SK_A><<<dim3(h.n_wg_a, c->B), NT, T::LDS, s>>>(
+        sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
+        h.sk_L[0], h.rounds_a, c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps);
+  } else {
+    if (h.n_wg_a == 0) return MMSBM_OK;
+    if ((rc = lds_opt_in(c, 6, &sk_pass_kernel<K, SK_LL>, T::LDS))) return rc;
+    sk_pass_kernel<K, SK_LL><<<dim3(h.n_wg_a, c->B), NT, T::LDS, s>>>(
+        sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
+        h.sk_L[0], h.rounds_a, c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps);
+  }
+  HIP_TRY(hipGetLastError());
+  return MMSBM_OK;
+}
+
+template <int K>
+int launch_sk_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, double* S,
+                  hipStream_t s) {
+  const SetDev& sd = c->sets[MMSBM_SET_TRAIN];
+  const auto& h = sd.h;
+  const int ngw = (c->P * K + SKF_NT - 1) / SKF_NT;
+  const int ncw = (K * K * K + SKF_CW - 1) / SKF_CW;
+  SpRange spr{};
+  for (int r = 0; r < c->R; ++r) {
+    spr.lo[r] = h.sp_lo[r];
+    spr.hi[r] = h.sp_hi[r];
+  }
+  const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
+  if (sums)
+    sk_fin_kernel<K, true><<<dim3(ngw + ncw, c->B), SKF_NT, 0, s>>>(
+        theta, pr, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
+        std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, nullptr, nullptr, 0);
+  else
+    sk_fin_kernel<K, false><<<dim3(ngw + ncw + nqc, c->B), SKF_NT, 0, s>>>(
+        theta, pr, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
+        std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg);
+  HIP_TRY(hipGetLastError());
+  return MMSBM_OK;
+}
+
+template <int K>
+constexpr PassFn sk_pass_fn() {
+  if constexpr (K <= 12) return &launch_sk_pass<K>;
+  else return nullptr;
+}
+template <int K>
+constexpr FinFn sk_fin_fn() {
+  if constexpr (K <= 12) return &launch_sk_fin<K>;
+  else return nullptr;
+}
+
 template <int... Ks>
 constexpr auto make_table(std::integer_sequence<int, Ks...>) {
   return std::array<Launch, sizeof...(Ks)>{Launch{&launch_pass<Ks + 1>, &launch_fin<Ks + 1>,
                                                   &launch_mapply<Ks + 1>, &launch_predict<Ks + 1>,
-                                                  KT<Ks + 1>::GMAX}...};
+                                                  KT<Ks + 1>::GMAX, sk_pass_fn<Ks + 1>(),
+                                                  sk_fin_fn<Ks + 1>()}...};
 }
 
+
 const auto kTable = make_table(std::make_integer_sequence<int, MMSBM_MAX_K>{});
+
+// the pass / fin launchers of this context (the small-K kernels of sk.h when c->sk)
+PassFn pass_of(const mmsbm_ctx* c) { return c->sk ? kTable[c->K - 1].sk_pass : kTable[c->K - 1].pass; }
+FinFn fin_of(const mmsbm_ctx* c) { return c->sk ? kTable[c->K - 1].sk_fin : kTable[c->K - 1].fin; }
 
 int gmax_for(int K) { return kTable[K - 1].gmax; }
 
@@ -1509,6 +1617,17 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
   c->B = B;
   c->P = P;
   c->eps = eps;
+  {
+    const char* e = getenv("MMSBM_SK");  // MMSBM_SK=0: the large-K kernels at every K (measurement)
+    const bool sk = K <= 12 && !(e && e[0] == '0');
+    if (sk != c->sk) {  // the plans are built for one kernel family
+      DeviceGuard g(c->device);
+      for (auto& sd : c->sets) sd.release();
+      c->ws = nullptr;
+      c->ws_bytes = 0;
+    }
+    c->sk = sk;
+  }
   ++c->gen;
   c->attr = 0;      // the dynamic-LDS opt-ins are per kernel, and the kernels depend on K
   c->warm = false;
@@ -1550,8 +1669,12 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
       units_b = b;
     }
   }
+  // small-K plans: about 1024 workgroups per stream group, units in rounds of NW beyond that;
+  // MMSBM_SK_WG=n lowers the target (tests: several rounds per workgroup)
+  int wg_target = 1024;
+  if (const char* v = getenv("MMSBM_SK_WG")) wg_target = std::max(1, atoi(v));
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
-                           c->gcap, c->K <= 12 ? 16 : 4 * c->K);
+                           c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, wg_target);
   const auto& h = sd.h;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;
@@ -1573,6 +1696,11 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   if ((rc = upload(&sd.prow_ptr, h.prow_ptr))) return rc;
   if ((rc = upload(&sd.prow_gene, h.prow_gene))) return rc;
   if ((rc = upload(&sd.sp_desc, h.sp_desc))) return rc;
+  for (int g = 0; g < 2; ++g) {
+    if ((rc = upload(&sd.sku[g], h.sk_udesc[g]))) return rc;
+    if ((rc = upload(&sd.skr[g], h.sk_urec[g]))) return rc;
+  }
+  if ((rc = upload(&sd.skrow12, h.sk_urow12))) return rc;
   sd.present = true;
   ++c->gen;
   c->ws = nullptr;  // the workspace layout changed: mmsbm_set_workspace again
@@ -1628,16 +1756,17 @@ int mmsbm_set_workspace(mmsbm_ctx* c, void* ws, int64_t bytes) {
 
 // One EM iteration = pass A, pass B, fin (theta / p in place).
 static int one_iteration(mmsbm_ctx* c, double* theta, double* pr, bool mark, hipStream_t s) {
-  const Launch& L = kTable[c->K - 1];
+  const PassFn pass = pass_of(c);
+  const FinFn fin = fin_of(c);
   int rc;
   if (mark && (rc = timing_mark(c, 0, s))) return rc;
-  if ((rc = L.pass(c, PASS_A, MMSBM_SET_TRAIN, theta, pr, s))) return rc;
+  if ((rc = pass(c, PASS_A, MMSBM_SET_TRAIN, theta, pr, s))) return rc;
   if (mark && (rc = timing_mark(c, 0, s))) return rc;
   if (mark && (rc = timing_mark(c, 1, s))) return rc;
-  if ((rc = L.pass(c, PASS_B, MMSBM_SET_TRAIN, theta, pr, s))) return rc;
+  if ((rc = pass(c, PASS_B, MMSBM_SET_TRAIN, theta, pr, s))) return rc;
   if (mark && (rc = timing_mark(c, 1, s))) return rc;
   if (mark && (rc = timing_mark(c, 2, s))) return rc;
-  if ((rc = L.fin(c, false, theta, pr, nullptr, nullptr, s))) return rc;
+  if ((rc = fin(c, false, theta, pr, nullptr, nullptr, s))) return rc;
   if (mark && (rc = timing_mark(c, 2, s))) return rc;
   c->warm = true;
   return MMSBM_OK;
@@ -1745,7 +1874,7 @@ int mmsbm_accumulate(mmsbm_ctx* c, const double* theta, const double* pr, double
   if (!theta || !pr || !nth || !S) return fail(MMSBM_ERR_INVALID, "null pointer");
   DeviceGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
-  const Launch& L = kTable[c->K - 1];
+  const PassFn pass = pass_of(c);
   double* th = const_cast<double*>(theta);  // the passes only read theta / pr; fin in sums mode
   double* p = const_cast<double*>(pr);      // writes nth / S and leaves them untouched
   if (c->sets[MMSBM_SET_TRAIN].h.n_obs == 0) {  // a rank without train links adds zeros
@@ -1757,9 +1886,9 @@ int mmsbm_accumulate(mmsbm_ctx* c, const double* theta, const double* pr, double
     HIP_TRY(hipMemsetAsync(S, 0, sizeof(double) * c->B * c->R * c->K * c->K * c->K, s));
     return MMSBM_OK;
   }
-  if ((rc = L.pass(c, PASS_A, MMSBM_SET_TRAIN, th, p, s))) return rc;
-  if ((rc = L.pass(c, PASS_B, MMSBM_SET_TRAIN, th, p, s))) return rc;
-  return L.fin(c, true, th, p, nth, S, s);
+  if ((rc = pass(c, PASS_A, MMSBM_SET_TRAIN, th, p, s))) return rc;
+  if ((rc = pass(c, PASS_B, MMSBM_SET_TRAIN, th, p, s))) return rc;
+  return fin_of(c)(c, true, th, p, nth, S, s);
 }
 
 int mmsbm_mstep(mmsbm_ctx* c, double* theta, double* pr, const double* nth, const double* S,
@@ -1792,7 +1921,7 @@ int mmsbm_loglik(mmsbm_ctx* c, int32_t which, const double* theta, const double*
     HIP_TRY(hipMemsetAsync(out, 0, sizeof(double) * c->B, s));
     return MMSBM_OK;
   }
-  if ((rc = kTable[c->K - 1].pass(c, PASS_LL, which, theta, pr, s))) return rc;
+  if ((rc = pass_of(c)(c, PASS_LL, which, theta, pr, s))) return rc;
   reduce_kernel<<<c->B, 256, 0, s>>>(c->partL, sd.h.n_wg_a, out);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
@@ -1859,9 +1988,11 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[4] = h.n_wg_b;
   info[5] = h.n_sp;
   info[6] = h.n_prows;
-  info[7] = h.gmax;
-  info[8] = (int64_t)h.vgenes.size();
   info[9] = h.prow_ptr.empty() ? 0 : h.prow_ptr[(size_t)h.R * (h.P + 1)];  // stream-0 partial rows
+  info[7] = h.small ? mmsbm_plan::GU : h.gmax;
+  info[8] = h.small ? info[9] : (int64_t)h.vgenes.size();  // small-K: one V table per stream-0 stretch
+  info[10] = h.small ? 1 : 0;
+  info[11] = h.small ? h.n_units : (int64_t)(h.n_wg_a + h.n_wg_b) * NW;
   return MMSBM_OK;
 }
 
@@ -1881,15 +2012,16 @@ int mmsbm_time_kernel(mmsbm_ctx* c, int32_t kernel, double* theta, double* pr, i
   if (rc) return rc;
   DeviceGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
-  const Launch& L = kTable[c->K - 1];
+  const PassFn pass = pass_of(c);
+  const FinFn fin = fin_of(c);
   hipEvent_t e0, e1;
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
   HIP_TRY(hipEventRecord(e0, s));
   // pass A / pass B only read theta / p; fin runs in sums mode into workspace scratch
   for (int i = 0; i < n && rc == MMSBM_OK; ++i)
-    rc = kernel == 2 ? L.fin(c, true, theta, pr, c->nth_tmp, c->S_tmp, s)
-                     : L.pass(c, kernel == 0 ? PASS_A : PASS_B, MMSBM_SET_TRAIN, theta, pr, s);
+    rc = kernel == 2 ? fin(c, true, theta, pr, c->nth_tmp, c->S_tmp, s)
+                     : pass(c, kernel == 0 ? PASS_A : PASS_B, MMSBM_SET_TRAIN, theta, pr, s);
   HIP_TRY(hipEventRecord(e1, s));
   HIP_TRY(hipEventSynchronize(e1));
   float ms = 0.f;

@@ -26,6 +26,12 @@ namespace mmsbm_plan {
 
 constexpr int CH = 4;   // observations per chunk (one MFMA k-step)
 constexpr int NW = 8;   // waves (units) per workgroup
+// Small-K plans (K <= 12, the register-direct kernels of sk.h): a unit has at most GU gene
+// stretches (one wave keeps their V tables and M rows, and contracts them with p at its end) and
+// at most LCAP_SK chunks (its records are staged in the wave's LDS at once).
+constexpr int GU = 4;
+constexpr int LCAP_SK = 32;
+constexpr int UD = 16;  // ints per unit descriptor (below)
 
 struct I4 {
   int x, y, z, w;
@@ -45,6 +51,29 @@ struct Plan {
   std::vector<int> prow_gene;      // [n_prows]
   std::vector<int> sp_desc;        // S-partial workgroups: [n_sp][3] (rating, prow begin, end)
   int sp_lo[8] = {0}, sp_hi[8] = {0};  // S-partial workgroups of each rating
+  // small-K plans only (sk.h):
+  bool small = false;
+  std::vector<int> udesc;          // [n_units][UD]: stretch start chunks [0..3], end chunk [4],
+                                   // stretches [5], partial rows [6..9], pivot genes [10..13],
+                                   // stream * 16 + rating [14]
+  std::vector<int> wg_ustart;      // [n_wg + 1] units of each workgroup (rounds of NW)
+  std::vector<int> row12;          // [n_rows0][2] the observation's stream-1 / stream-2 row
+                                   // (relative to n_rows0; -1 on padding rows)
+  int rounds_a = 1, rounds_b = 1;  // unit rounds per workgroup (stream 0 / streams 1, 2)
+  long long n_units = 0;
+  // slot layout the small-K kernels read (make_slots below); group 0 = stream 0 (pass A), group 1 =
+  // streams 1, 2 (pass B).  Workgroup w of a group owns slots [w rounds NW, (w + 1) rounds NW) (round
+  // major, then wave); a slot holds one unit or nothing.  Records are copied slot-major with a fixed
+  // capacity of 4 L rows per slot, so a wave finds its unit's records from its slot number alone.
+  int sk_L[2] = {0, 0};            // chunks per slot (the group's longest unit)
+  long long sk_slots[2] = {0, 0};
+  std::vector<int> sk_udesc[2];    // [slots][UD]: stretch starts [0..3] and end [4] relative to the
+                                   // slot's first chunk, stretches [5] (0: empty slot), partial rows
+                                   // [6..9], pivot genes [10..13], stream * 16 + rating [14]
+  std::vector<I4> sk_urec[2];      // [slots][4 L] records
+  std::vector<int> sk_urow12;      // [slots_0][4 L][2] slot-major row of the stream-1 / stream-2 copy
+                                   // of each stream-0 row (-1: padding), the index of its c in pass B
+  int sk_wg_end[3 * 8] = {0};      // section (s, r) = s R + r ends at workgroup sk_wg_end[s R + r]
   int n_wg_a = 0;                  // stream-0 workgroups (the first n_wg_a)
   int n_wg_b = 0;                  // stream-1/2 workgroups (the next n_wg_b)
   int n_sp = 0;
@@ -83,16 +112,80 @@ inline void pack_units(const std::vector<int>& run_chunks, int lmax, int gcap, s
   if (cur > 0) ub.push_back(pos);
 }
 
+// Slot layout of a small-K plan (see Plan::sk_*), from the per-unit descriptors and row12.
+inline void make_slots(Plan& pl) {
+  const int R = pl.R;
+  const int n_wg = (int)pl.wg_code.size();
+  // section ends
+  {
+    int sec = 0;
+    for (int w = 0; w < n_wg; ++w) {
+      const int code = (pl.wg_code[w] >> 4) * R + (pl.wg_code[w] & 15);
+      while (sec < code) pl.sk_wg_end[sec++] = w;
+    }
+    while (sec < 3 * R) pl.sk_wg_end[sec++] = n_wg;
+  }
+  std::vector<long long> pos(pl.rows.size(), -1);  // slot-major position of every real row
+  for (int g = 0; g < 2; ++g) {
+    const int w0 = g == 0 ? 0 : pl.n_wg_a, w1 = g == 0 ? pl.n_wg_a : n_wg;
+    const int per = NW * (g == 0 ? pl.rounds_a : pl.rounds_b);
+    int L = 1;
+    for (int w = w0; w < w1; ++w)
+      for (int u = pl.wg_ustart[w]; u < pl.wg_ustart[w + 1]; ++u) {
+        const int* d = &pl.udesc[(size_t)u * UD];
+        L = std::max(L, d[4] - d[0]);
+      }
+    pl.sk_L[g] = L;
+    pl.sk_slots[g] = (long long)(w1 - w0) * per;
+    pl.sk_udesc[g].assign((size_t)pl.sk_slots[g] * UD, 0);
+    pl.sk_urec[g].assign((size_t)pl.sk_slots[g] * 4 * L, I4{0, 0, 0, 0});
+    for (int w = w0; w < w1; ++w)
+      for (int k = 0; k < per; ++k) {
+        const long long slot = (long long)(w - w0) * per + k;
+        int* sd = &pl.sk_udesc[g][(size_t)slot * UD];
+        const int u = pl.wg_ustart[w] + k;
+        if (u >= pl.wg_ustart[w + 1]) {  // empty slot
+          sd[14] = pl.wg_code[w];
+          continue;
+        }
+        const int* d = &pl.udesc[(size_t)u * UD];
+        const int c0 = d[0];
+        for (int t = 0; t < UD; ++t) sd[t] = d[t];
+        for (int t = 0; t < 5; ++t) sd[t] = d[t] - c0;
+        I4* rec = &pl.sk_urec[g][(size_t)slot * 4 * L];
+        const long long row0 = 4LL * c0, nrow = 4LL * (d[4] - c0);
+        for (long long i = 0; i < 4LL * L; ++i) {
+          const long long row = row0 + (i < nrow ? i : nrow - 1);  // padding: the unit's last row
+          rec[i] = pl.rows[row];
+          if (i < nrow) pos[row] = slot * 4 * L + i;
+        }
+      }
+  }
+  if (!pl.row12.empty()) {
+    const int L = pl.sk_L[0];
+    pl.sk_urow12.assign((size_t)pl.sk_slots[0] * 4 * L * 2, -1);
+    for (long long q = 0; q < pl.n_rows0; ++q) {
+      if (pos[q] < 0) continue;
+      for (int k = 0; k < 2; ++k) {
+        const int t = pl.row12[(size_t)2 * q + k];
+        pl.sk_urow12[(size_t)2 * pos[q] + k] = t < 0 ? -1 : (int)pos[pl.n_rows0 + t];
+      }
+    }
+  }
+}
+
 // Builds the plan.  units_a / units_b: the number of units to aim for in stream 0 and in streams
 // 1 + 2 together (about 8 waves per CU); gcap: most distinct genes per stream-0 workgroup (its
 // V table lives in LDS); sp_rows: stream-0 partial rows per S-partial workgroup (each writes a
 // K^3 partial, so large K wants more rows per partial).
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
-                  int units_a, int units_b, int gcap, int sp_rows = 16) {
+                  int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
+                  int wg_target = 1024) {
   Plan pl;
   pl.R = R;
   pl.P = P;
   pl.streams = em ? 3 : 1;
+  pl.small = small;
   // observations of each rating in link order
   std::vector<std::vector<int>> obs(R);
   for (long long e = 0; e < E; ++e)
@@ -135,9 +228,15 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   // unit length: the work spread over about units_* units, but no unit longer than LCAP chunks
   // (large link sets get more units rather than longer ones, so a few long units do not set
   // the kernel's duration)
-  constexpr long long LCAP = 64;
+  const long long LCAP = small ? LCAP_SK : 64;
   const int lmax_a = (int)std::min(LCAP, std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1)));
   const int lmax_b = (int)std::min(LCAP, std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1)));
+  if (small) {  // unit rounds per workgroup: about wg_target workgroups per stream group
+    const long long ua = (chunks_a + lmax_a - 1) / lmax_a, ub_ = (chunks_b + lmax_b - 1) / lmax_b;
+    pl.rounds_a = (int)std::max<long long>(1, (ua + (long long)NW * wg_target - 1) / ((long long)NW * wg_target));
+    pl.rounds_b = (int)std::max<long long>(1, (ub_ + (long long)NW * wg_target - 1) / ((long long)NW * wg_target));
+    pl.wg_ustart.push_back(0);
+  }
 
   std::vector<int> wg_stream;
   for (int s = 0; s < pl.streams; ++s) {
@@ -171,7 +270,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       }
       // units
       std::vector<int> ub;
-      pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, s == 0 ? gcap : (1 << 30), ub);
+      pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? GU : s == 0 ? gcap : (1 << 30), ub);
       const int nunits = (int)ub.size() - 1;
       // chunk -> gene
       const int nch = ub.empty() ? 0 : ub.back();
@@ -181,48 +280,81 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
         for (size_t k = 0; k < run_chunks.size(); ++k)
           for (int t = 0; t < run_chunks[k]; ++t) cgene[c++] = run_gene[k];
       }
-      // workgroups: NW consecutive units; stream 0 also caps the distinct genes (V table)
-      std::vector<int> wstart;  // unit index where each workgroup starts
-      {
-        int u = 0;
-        while (u < nunits) {
-          wstart.push_back(u);
-          int taken = 0, genes = 0, last = -1;
-          while (u < nunits && taken < NW) {
-            int ug = 0, lg = last;
-            for (int c = ub[u]; c < ub[u + 1]; ++c)
-              if (cgene[c] != lg) {
-                ++ug;
-                lg = cgene[c];
-              }
-            if (s == 0 && taken > 0 && genes + ug > gcap) break;
-            genes += ug;
-            last = lg;
-            ++taken;
-            ++u;
+      if (small) {
+        // workgroups: rounds of NW consecutive units of this (stream, rating); unit descriptors
+        const int per = NW * (s == 0 ? pl.rounds_a : pl.rounds_b);
+        const long long u_first = pl.n_units;
+        for (int u = 0; u < nunits; ++u) {
+          int d[UD];
+          const int c0 = ub[u], c1 = ub[u + 1];
+          int nst = 0;
+          for (int c = c0; c < c1; ++c)
+            if (c == c0 || cgene[c] != cgene[c - 1]) {
+              d[nst] = chunk_base + c;      // stretch start
+              d[10 + nst] = cgene[c];       // its pivot gene
+              ++nst;
+            }
+          for (int t = nst; t < GU; ++t) {
+            d[t] = chunk_base + c1;
+            d[10 + t] = cgene[c0];
+          }
+          d[4] = chunk_base + c1;
+          d[5] = nst;
+          for (int t = 0; t < GU; ++t) d[6 + t] = -1;  // partial rows: filled below (em plans)
+          d[14] = s * 16 + r;
+          d[15] = 0;
+          pl.udesc.insert(pl.udesc.end(), d, d + UD);
+        }
+        pl.n_units += nunits;
+        for (int u = 0; u < nunits; u += per) {
+          pl.wg_ustart.push_back((int)(u_first + std::min(u + per, nunits)));
+          pl.wg_code.push_back(s * 16 + r);
+          wg_stream.push_back(s);
+        }
+      } else {
+        // workgroups: NW consecutive units; stream 0 also caps the distinct genes (V table)
+        std::vector<int> wstart;  // unit index where each workgroup starts
+        {
+          int u = 0;
+          while (u < nunits) {
+            wstart.push_back(u);
+            int taken = 0, genes = 0, last = -1;
+            while (u < nunits && taken < NW) {
+              int ug = 0, lg = last;
+              for (int c = ub[u]; c < ub[u + 1]; ++c)
+                if (cgene[c] != lg) {
+                  ++ug;
+                  lg = cgene[c];
+                }
+              if (s == 0 && taken > 0 && genes + ug > gcap) break;
+              genes += ug;
+              last = lg;
+              ++taken;
+              ++u;
+            }
           }
         }
-      }
-      for (size_t w = 0; w < wstart.size(); ++w) {
-        const int u0 = wstart[w];
-        const int u1 = w + 1 < wstart.size() ? wstart[w + 1] : nunits;
-        for (int i = 0; i <= NW; ++i) {
-          const int u = std::min(u0 + i, u1);
-          pl.wg_units.push_back(chunk_base + ub[u]);
-        }
-        pl.wg_code.push_back(s * 16 + r);
-        wg_stream.push_back(s);
-        if (s == 0) {
-          pl.wg_gene.push_back((int)pl.vgenes.size());
-          const int first = (int)pl.vgenes.size();
-          for (int c = ub[u0]; c < ub[u1]; ++c)
-            if ((int)pl.vgenes.size() == first || pl.vgenes.back() != cgene[c]) pl.vgenes.push_back(cgene[c]);
-          for (int c = ub[u0]; c < ub[u1]; ++c) {
-            // genes ascend within the stream, so the slot is a lower_bound in this list
-            const auto it = std::lower_bound(pl.vgenes.begin() + first, pl.vgenes.end(), cgene[c]);
-            pl.chunk_vslot.push_back((int)(it - (pl.vgenes.begin() + first)));
+        for (size_t w = 0; w < wstart.size(); ++w) {
+          const int u0 = wstart[w];
+          const int u1 = w + 1 < wstart.size() ? wstart[w + 1] : nunits;
+          for (int i = 0; i <= NW; ++i) {
+            const int u = std::min(u0 + i, u1);
+            pl.wg_units.push_back(chunk_base + ub[u]);
           }
-          pl.gmax = std::max(pl.gmax, (int)pl.vgenes.size() - first);
+          pl.wg_code.push_back(s * 16 + r);
+          wg_stream.push_back(s);
+          if (s == 0) {
+            pl.wg_gene.push_back((int)pl.vgenes.size());
+            const int first = (int)pl.vgenes.size();
+            for (int c = ub[u0]; c < ub[u1]; ++c)
+              if ((int)pl.vgenes.size() == first || pl.vgenes.back() != cgene[c]) pl.vgenes.push_back(cgene[c]);
+            for (int c = ub[u0]; c < ub[u1]; ++c) {
+              // genes ascend within the stream, so the slot is a lower_bound in this list
+              const auto it = std::lower_bound(pl.vgenes.begin() + first, pl.vgenes.end(), cgene[c]);
+              pl.chunk_vslot.push_back((int)(it - (pl.vgenes.begin() + first)));
+            }
+            pl.gmax = std::max(pl.gmax, (int)pl.vgenes.size() - first);
+          }
         }
       }
       if (s != 0) pl.chunk_vslot.resize(pl.chunk_vslot.size() + nch, 0);
@@ -238,6 +370,13 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
             ++pl.n_prows;
           }
           pl.chunk_prow.push_back((int)(pl.n_prows - 1));
+        }
+        if (small) {  // each unit stretch's partial row
+          const long long u_first = pl.n_units - (long long)(ub.size() - 1);
+          for (int u = 0; u + 1 < (int)ub.size(); ++u) {
+            int* d = &pl.udesc[(size_t)(u_first + u) * UD];
+            for (int t = 0; t < d[5]; ++t) d[6 + t] = pl.chunk_prow[(size_t)d[t]];
+          }
         }
         // CSR over genes: prows of stream (s, r) ascend by gene
         std::vector<int> cnt(P + 1, 0);
@@ -261,6 +400,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
           q = q1;
         }
         pl.n_rows0 = (long long)pl.rows.size();
+        if (small && em) pl.row12.resize((size_t)2 * pl.n_rows0, -1);
       } else {
         // c index of every row of this stream section
         size_t rr = (size_t)row_base;
@@ -268,7 +408,11 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
           const int g = ids[(size_t)o[q] * 3 + s];
           size_t q1 = q;
           while (q1 < o.size() && ids[(size_t)o[q1] * 3 + s] == g) ++q1;
-          for (size_t t = q; t < q1; ++t) pl.rows[rr++].w = row0[r][o[t]];
+          for (size_t t = q; t < q1; ++t) {
+            const int r0 = row0[r][o[t]];
+            if (small) pl.row12[(size_t)2 * r0 + (s - 1)] = (int)((long long)rr - pl.n_rows0);
+            pl.rows[rr++].w = r0;
+          }
           const int pad = (CH - (int)(q1 - q) % CH) % CH;
           for (int t = 0; t < pad; ++t) pl.rows[rr++].w = -2;
           q = q1;
@@ -281,6 +425,22 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   pl.wg_gene.push_back((int)pl.vgenes.size());
   for (auto& rec : pl.rows)
     if (rec.w == -2) rec.w = (int)pl.n_rows0;  // padding rows of streams 1, 2: the zero c slot
+  if (small) {
+    // S partials: one per stream-0 workgroup; those of rating r are workgroups [sp_lo, sp_hi)
+    for (int r = 0; r < R; ++r) {
+      pl.sp_lo[r] = pl.sp_hi[r] = 0;
+      bool seen = false;
+      for (int w = 0; w < pl.n_wg_a; ++w)
+        if ((pl.wg_code[w] & 15) == r) {
+          if (!seen) pl.sp_lo[r] = w;
+          seen = true;
+          pl.sp_hi[r] = w + 1;
+        }
+    }
+    pl.n_sp = pl.n_wg_a;
+    make_slots(pl);
+    return pl;
+  }
   // S-partial workgroups over the stream-0 partial rows of each rating
   if (em) {
     for (int r = 0; r < R; ++r) {

@@ -1,0 +1,548 @@
+// sk.h — the small-K (K <= 12) EM kernels of mmsbm.hip: one EM iteration
+// (src/TrigenicInteractionPredictor.py make_iteration :984-1043) as sk_pass_kernel<K, SK_A>,
+// sk_pass_kernel<K, SK_B> and sk_fin_kernel<K>; compute_likelihood (:952-974) as
+// sk_pass_kernel<K, SK_LL> + reduce_kernel.  Same pivot-run algebra as the large-K kernels
+// (mmsbm.hip header), laid out for latency instead of throughput:
+//
+//  * one unit (<= GU gene stretches, <= LCAP_SK chunks of 4 observations) per wave, and no
+//    workgroup barrier between a wave's start and its end: the wave stages its unit's records in
+//    its own LDS with one coalesced load, computes the V tables of its own <= 4 pivot genes
+//    (one MFMA per (a tile, cell group), p_r staged once per workgroup), and gathers the theta
+//    values of every chunk straight into the registers its MFMA operands need, SKD chunks ahead;
+//  * a gene stretch's M row (K x K) never leaves the wave: at the unit's end the wave contracts
+//    its <= 4 rows with p (X, K values per row, one MFMA per cell step) and, on stream 0, forms
+//    its share of S = sum_g theta_g (x) M0_g in registers; a workgroup adds its 8 waves' S in a
+//    fixed order and writes ONE K^3 partial;
+//  * pass A stores each observation's c = n / d at its stream-1 and stream-2 rows (plan row12),
+//    so pass B reads c coalesced with its records;
+//  * fin sums the X partials per gene (theta update) and the S partials per cell (p update).
+// Bytes per iteration: records + c + X partials (K per partial row) + S partials (K^3 per stream-0
+// workgroup), against K^2 per partial row written and read back by the large-K path.
+//
+// MFMA lane maps as in mmsbm.hip: v_mfma_f64_4x4x4f64 (lane = 16 hi + 4 blk + lo) takes
+// A[blk][m = lo][k = hi], B[blk][k = hi][n = lo] and gives D[blk][m = hi][n = lo];
+// v_mfma_f64_16x16x4f64 takes A[m = l & 15][k = l >> 4], B[k = l >> 4][n = l & 15] and gives
+// D[m = (l >> 4) + 4 i][n = l & 15] in element i.
+
+enum { SK_A = 0, SK_LL = 1, SK_B = 2 };
+
+constexpr int SKD = 3;                 // chunks of theta gathers in flight ahead of the compute
+constexpr int SK_ROWS = 4 * mmsbm_plan::LCAP_SK;  // records staged per wave (one unit)
+
+template <int K>
+struct SKT {
+  static constexpr int NG = (K + 3) / 4;          // 4-wide tiles of one K axis (<= 3)
+  static constexpr int K2 = K * K, K3 = K * K * K;
+  static constexpr int NCT = (K2 + 3) / 4;        // 4-cell tiles of a dense K x K row
+  static constexpr int NCG = (NCT + 3) / 4;       // groups of 4 cell tiles (one MFMA, 4 blocks)
+  static constexpr int SLOT = 4 * NCT;            // doubles per stretch slot (V table, then M row)
+  static constexpr int PSD = (K3 + 1) & ~1;       // staged p_r (16-B aligned)
+  static constexpr int WAVE = mmsbm_plan::GU * SLOT + 2 * SK_ROWS + SK_ROWS;  // slots, records, aux
+  static constexpr int NS = NG * NCG;             // S accumulators per lane
+  static constexpr int LDS = (PSD + NW * WAVE) * 8;
+  static_assert(K <= 12, "small-K kernels: K <= 12");
+  static_assert(4 * NS * 64 <= PSD + NW * WAVE, "S reduction buffer over the LDS");
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+};
+
+// p index of P^s[z][cell] (s = the pivot slot z sits in; cell = x K + y over the two other
+// slots u, v in order): s = 0 p[z][x][y], s = 1 p[x][z][y], s = 2 p[x][y][z]
+template <int K>
+__device__ __forceinline__ int sk_pidx(int s, int z, int x, int y) {
+  return s == 0 ? (z * K + x) * K + y : s == 1 ? (x * K + z) * K + y : (x * K + y) * K + z;
+}
+
+struct SkSec {  // workgroup sections of a small-K plan (Plan::sk_wg_end)
+  int wg_end[3 * MAX_R];
+};
+
+// grid (the group's workgroups, B), block 512; group 0 (SK_A, SK_LL) = stream 0, group 1 (SK_B) =
+// streams 1 and 2.  Workgroup w owns unit slots [w rounds NW, (w + 1) rounds NW) (Plan::sk_*).
+template <int K, int MODE>
+__global__ __launch_bounds__(NT) void sk_pass_kernel(
+    const int4* __restrict__ urec, const int* __restrict__ udesc, const int2* __restrict__ urow12,
+    const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ cB,
+    double* __restrict__ xpart, double* __restrict__ spart, double* __restrict__ partL, SkSec sec,
+    int wg_base, int L, int rounds, int P, int R, long long n_cb, long long n_prows, int n_wg,
+    double eps) {
+  using T = SKT<K>;
+  constexpr int NG = T::NG, K2 = T::K2, K3 = T::K3, NCT = T::NCT, NCG = T::NCG, SLOT = T::SLOT;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3, col = lane & 15;
+  const int w = blockIdx.x, b = blockIdx.y;
+  int sr = 0;  // this workgroup's (stream, rating) section, from the launch arguments alone
+  while (sr + 1 < 3 * R && wg_base + w >= sec.wg_end[sr]) ++sr;
+  const int s = sr / R, r = sr % R;
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+  const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
+  double* Ps = smem;
+  double* wl = smem + T::PSD + wv * T::WAVE;
+  double* MSl = wl;                                                 // GU slots: V, then M
+  int4* REC = reinterpret_cast<int4*>(wl + mmsbm_plan::GU * SLOT);  // the unit's records
+  double* AUX = wl + mmsbm_plan::GU * SLOT + 2 * SK_ROWS;           // row12 (A) / c (B)
+  double* __restrict__ cBb = cB + (size_t)b * n_cb;
+  double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
+  Stamp st_{};
+  st_.mark(0);
+
+  // One slot's descriptor, records (+ row12 / c) and pivot-gene theta, loaded together.  The
+  // first round's loads are issued before the p staging below, so they share its round trip.
+  struct Unit {
+    int nst, d1, d2, d3, c1, prow;
+    int4 rv[2];
+    int2 r12[2];
+    double cv[2];
+    double tv[NG], ts[NG];  // theta_{gene lo}[4 as + hi] (V), theta_{gene hi}[4 at + lo] (S)
+  };
+  auto load_unit = [&](int rd, Unit& un) {
+    const long long slot = ((long long)w * rounds + rd) * NW + wv;
+    const int* __restrict__ d = udesc + slot * mmsbm_plan::UD;
+    un.nst = d[5];
+    un.d1 = d[1];
+    un.d2 = d[2];
+    un.d3 = d[3];
+    un.c1 = d[4];
+    un.prow = d[6 + hi];
+    const int nrow = 4 * un.c1 > 0 ? 4 * un.c1 : 1;
+    const long long rbase = slot * 4 * L;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = lane + 64 * i;
+      const long long row = rbase + (idx < nrow ? idx : nrow - 1);
+      un.rv[i] = urec[row];
+      if constexpr (MODE == SK_A) un.r12[i] = urow12[row];
+      if constexpr (MODE == SK_B) un.cv[i] = cBb[row];
+    }
+    if constexpr (MODE != SK_B) {
+      const int glo = d[10 + lo], ghi = d[10 + hi];
+#pragma unroll
+      for (int as = 0; as < NG; ++as) {
+        const int a1 = 4 * as + hi, a2 = 4 * as + lo;
+        const double v1 = th[(size_t)glo * K + (a1 < K ? a1 : 0)];
+        const double v2 = th[(size_t)ghi * K + (a2 < K ? a2 : 0)];
+        un.tv[as] = (lo < un.nst && a1 < K) ? v1 : 0.0;
+        un.ts[as] = (hi < un.nst && a2 < K) ? v2 : 0.0;
+      }
+    }
+  };
+  Unit un;
+  load_unit(0, un);
+
+  // p_r staged once per workgroup (every unit of a workgroup has its rating)
+  {
+    constexpr int NPI = (K3 + NT - 1) / NT;
+    double pv[NPI];
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) pv[i] = p[tid + NT * i < K3 ? tid + NT * i : 0];
+#pragma unroll
+    for (int i = 0; i < NPI; ++i)
+      if (tid + NT * i < K3) Ps[tid + NT * i] = pv[i];
+  }
+  __syncthreads();
+  st_.mark(6);
+
+  double sacc[NG][NCG];  // SK_A: this wave's share of S_r[a][cell], a = 4 at + hi
+#pragma unroll
+  for (int at = 0; at < NG; ++at)
+#pragma unroll
+    for (int cg = 0; cg < NCG; ++cg) sacc[at][cg] = 0.0;
+  double ll = 0.0;
+
+  for (int rd = 0; rd < rounds; ++rd) {
+    if (rd > 0) load_unit(rd, un);
+    const int nst = un.nst;
+    if (nst == 0) continue;  // an empty slot (no barrier in the round loop)
+    const int c0 = 0, d1 = un.d1, d2 = un.d2, d3 = un.d3, c1 = un.c1;
+    st_.t[5] = (unsigned long long)(c1 - c0);
+    st_.t[4] = (unsigned long long)nst;
+    auto stretch_end = [&](int t) {  // first chunk after stretch t
+      return t + 1 >= nst ? c1 : t == 0 ? d1 : t == 1 ? d2 : d3;
+    };
+    const double* tv = un.tv;
+    const double* ts = un.ts;
+    const int4* rv = un.rv;
+    const int2* r12 = un.r12;
+    const double* cv = un.cv;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = lane + 64 * i;
+      REC[idx] = rv[i];
+      if constexpr (MODE == SK_A) reinterpret_cast<int2*>(AUX)[idx] = r12[i];
+      if constexpr (MODE == SK_B) AUX[idx] = cv[i];
+    }
+    if constexpr (MODE != SK_B) {
+      // ---- V_g[cell] = sum_a theta_g[a] p_r[a][cell] for the unit's genes (m = gene, k = a),
+      // into slot g of the wave's LDS (cell = b K + h)
+#pragma unroll
+      for (int cg = 0; cg < NCG; ++cg) {
+        const int cell = 4 * (4 * cg + blk) + lo;
+        double v = 0.0;
+#pragma unroll
+        for (int as = 0; as < NG; ++as) {
+          const int a = 4 * as + hi;
+          const bool ok = a < K && cell < K2;
+          const double pv = Ps[ok ? a * K2 + cell : 0];
+          v = mfma4(tv[as], ok ? pv : 0.0, v);
+        }
+        if (hi < nst && cell < K2) MSl[hi * SLOT + cell] = v;
+      }
+    }
+    wave_lds_sync();
+    st_.mark(1);
+
+    // ---- chunk loop.  Stretch t = [d[t], d[t + 1]) (the last ends at c1) uses slot t: its V
+    // table while it runs, its M row once it is done.
+    const int4* __restrict__ rec = REC;
+    auto rec_at = [&](int q, int o) { return rec[(q - c0) * 4 + o]; };
+    // theta gathers of one chunk, straight into MFMA operand registers (addresses clamped, every
+    // load unconditional; the values are masked where they are used)
+    struct Ga {
+      double z[NG];  // A: Z: theta_k(obs lo)[4 hs + hi]
+      double a, v;   // M: theta_u(obs hi)[col], theta_v(obs hi)[col]
+    };
+    const int colc = col < K ? col : K - 1;
+    auto gather = [&](int q, Ga& g) {
+      const int4 rh = rec_at(q, hi);
+      const int gu = s == 0 ? rh.y : rh.x;          // u slot: j on stream 0, i on streams 1 / 2
+      const int gvv = s == 2 ? rh.y : rh.z;         // v slot: k, except j on stream 2
+      g.a = th[(size_t)gu * K + colc];
+      g.v = th[(size_t)gvv * K + colc];
+      if constexpr (MODE != SK_B) {
+        const int kl = rec_at(q, lo).z;
+#pragma unroll
+        for (int hs = 0; hs < NG; ++hs) {
+          const int h = 4 * hs + hi;
+          g.z[hs] = th[(size_t)kl * K + (h < K ? h : 0)];
+        }
+      }
+    };
+    double vb[NG];  // B of Z: V_t[b = col][h = 4 hs + hi]
+    auto load_v = [&](int t) {
+#pragma unroll
+      for (int hs = 0; hs < NG; ++hs) {
+        const int h = 4 * hs + hi;
+        const bool ok = col < K && h < K;
+        const double x = MSl[t * SLOT + (ok ? col * K + h : 0)];
+        vb[hs] = ok ? x : 0.0;
+      }
+    };
+    d4v m16 = d4v{0.0, 0.0, 0.0, 0.0};
+    int t = 0;
+    int send = stretch_end(0);
+    if constexpr (MODE != SK_B) load_v(0);
+    constexpr int U = SKD + 1;
+    Ga ring[U];
+#pragma unroll
+    for (int i = 0; i < SKD; ++i) gather(c0 + i < c1 ? c0 + i : c1 - 1, ring[i]);
+    const bool kcol = col < K;
+    for (int q0 = c0; q0 < c1; q0 += U) {
+#pragma unroll
+      for (int ph = 0; ph < U; ++ph) {
+        const int q = q0 + ph;
+        if (q >= c1) break;
+        gather(q + SKD < c1 ? q + SKD : c1 - 1, ring[(ph + SKD) % U]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the gathers SKD chunks ahead of their use
+        const Ga& g = ring[ph];
+        const int4 rh = rec_at(q, hi);
+        double c;
+        if constexpr (MODE != SK_B) {
+          // Z[obs hi][b = col] = sum_h theta_k(obs hi)[h] V[b][h]; d = eps + sum_b theta_j[b] Z[b]
+          double z = 0.0;
+#pragma unroll
+          for (int hs = 0; hs < NG; ++hs) z = mfma4(4 * hs + hi < K ? g.z[hs] : 0.0, vb[hs], z);
+          const double dd = row16_sum((kcol ? g.a : 0.0) * z) + eps;
+          if constexpr (MODE == SK_LL) {
+            if (col == 0) ll += (double)rh.w * log(dd);
+          } else {
+            c = (double)rh.w / dd;
+            if (col == 0) {
+              const int2 rr = reinterpret_cast<const int2*>(AUX)[(q - c0) * 4 + hi];
+              if (rr.x >= 0) {
+                st_wt(cBb + rr.x, c);
+                st_wt(cBb + rr.y, c);
+              }
+            }
+          }
+        } else {
+          c = AUX[(q - c0) * 4 + hi];
+        }
+        if constexpr (MODE != SK_LL) {
+          // M += c theta_u (x) theta_v over the chunk's 4 observations (k = observation)
+          m16 = mfma16(kcol ? g.a : 0.0, kcol ? c * g.v : 0.0, m16);
+          if (q + 1 == send) {  // stretch t done: its M row into slot t
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int x = hi + 4 * i;
+              if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
+            }
+            m16 = d4v{0.0, 0.0, 0.0, 0.0};
+            ++t;
+            send = stretch_end(t);
+            if constexpr (MODE == SK_A)
+              if (t < nst) load_v(t);
+          }
+        } else {
+          if (q + 1 == send) {
+            ++t;
+            send = stretch_end(t);
+            if (t < nst) load_v(t);
+          }
+        }
+      }
+    }
+    st_.mark(2);
+    if constexpr (MODE != SK_LL) {
+      wave_lds_sync();
+      // ---- X_q[z] = sum_cell P^s[z][cell] M_q[cell] for the unit's rows q (m = q, n = z in the
+      // block's z tile, k = 4 cells per step)
+      // (four independent accumulator chains over the cell steps, added in a fixed order)
+      double xa[4] = {0.0, 0.0, 0.0, 0.0};
+      const int z = 4 * blk + lo;
+#pragma unroll
+      for (int ks = 0; ks < NCT; ++ks) {
+        const int cell = 4 * ks + hi;
+        const bool cok = cell < K2;
+        const double am = MSl[(lo < nst && cok ? lo * SLOT + cell : 0)];
+        const int x = cok ? cell / K : 0, y = cok ? cell % K : 0;
+        const bool pok = blk < NG && z < K && cok;
+        const double bp = Ps[pok ? sk_pidx<K>(s, z, x, y) : 0];
+        xa[ks & 3] = mfma4((lo < nst && cok) ? am : 0.0, pok ? bp : 0.0, xa[ks & 3]);
+      }
+      const double xacc = (xa[0] + xa[1]) + (xa[2] + xa[3]);
+      if (hi < nst && blk < NG && z < K) st_wt(xb + (size_t)un.prow * K + z, xacc);
+      if constexpr (MODE == SK_A) {
+        // ---- S_r[a][cell] += sum_q theta_{g_q}[a] M_q[cell] (m = a, k = q, n = cell)
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) {
+          const int cell = 4 * (4 * cg + blk) + lo;
+          const bool ok = hi < nst && cell < K2;
+          const double mb = MSl[ok ? hi * SLOT + cell : 0];
+#pragma unroll
+          for (int at = 0; at < NG; ++at) sacc[at][cg] = mfma4(ts[at], ok ? mb : 0.0, sacc[at][cg]);
+        }
+      }
+      st_.mark(3);
+    }
+    wave_lds_sync();  // the next unit overwrites the records and slots
+  }
+
+  if constexpr (MODE == SK_A) {
+    // ---- the workgroup's S partial: the 8 waves' shares added in a fixed order,
+    // ((w0 + w4) + (w2 + w6)) + ((w1 + w5) + (w3 + w7)), through LDS
+    double* red = smem;
+    auto put = [&](int slot) {
+#pragma unroll
+      for (int at = 0; at < NG; ++at)
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) red[((slot * NG + at) * NCG + cg) * 64 + lane] = sacc[at][cg];
+    };
+    auto add = [&](int slot) {
+#pragma unroll
+      for (int at = 0; at < NG; ++at)
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) sacc[at][cg] += red[((slot * NG + at) * NCG + cg) * 64 + lane];
+    };
+    __syncthreads();
+    if (wv >= 4) put(wv - 4);
+    __syncthreads();
+    if (wv < 4) add(wv);
+    __syncthreads();
+    if (wv == 2 || wv == 3) put(wv - 2);
+    __syncthreads();
+    if (wv < 2) add(wv);
+    __syncthreads();
+    if (wv == 1) put(0);
+    __syncthreads();
+    if (wv == 0) {
+      add(0);
+      double* __restrict__ out = spart + ((size_t)b * n_wg + w) * K3;
+#pragma unroll
+      for (int at = 0; at < NG; ++at)
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) {
+          const int a = 4 * at + hi, cell = 4 * (4 * cg + blk) + lo;
+          if (a < K && cell < K2) st_wt(out + a * K2 + cell, sacc[at][cg]);
+        }
+    }
+  }
+  if constexpr (MODE == SK_LL) {
+    __shared__ double redl[NW];
+    ll = wave_sum(ll);
+    __syncthreads();
+    if (lane == 0) redl[wv] = ll;
+    __syncthreads();
+    if (tid == 0) {
+      double tt = 0.0;
+      for (int q = 0; q < NW; ++q) tt += redl[q];
+      partL[(size_t)b * n_wg + w] = tt;
+    }
+  }
+  st_.mark(7);
+  st_.flush(MODE == SK_B ? 1 : MODE == SK_A ? 0 : 4, ((long long)b * gridDim.x + w) * NW + wv, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// sk_fin_kernel, grid (gene workgroups + cell workgroups + q workgroups, B), block 256.
+//   gene part: thread (g, x): X = sum over the 3 R (stream, rating) combos of g's X partials, in
+//     combo then row order (+ the joint model's pair sums); theta' = theta X / deg (:1016-1018)
+//     or, SUMS, nth = X.
+//   cell part: 16 cells x 16 parts per workgroup: S_r[cell] = sum of the rating's S partials
+//     (one per stream-0 workgroup), parts combined in order; p' = p S / (eps + sum_r p S)
+//     (:1021-1028) in place, or, SUMS, S_out = S.
+//   q part (joint model): as in fin_kernel.
+// ------------------------------------------------------------------------------------------
+constexpr int SKF_NT = 256, SKF_CW = 16, SKF_NPART = 16;
+
+// sum of gene g's X partials (component x) over the combos c < nc, combo then row order; the
+// first row of every combo is loaded with all of them in flight
+template <int NCC>
+__device__ __forceinline__ double sk_gene_sum(const double* __restrict__ xb, const int* __restrict__ prow_ptr,
+                                              int P, int g, int x, int K, int nc) {
+  int qa[NCC], qb[NCC];
+#pragma unroll
+  for (int c = 0; c < NCC; ++c) {
+    const int cc = c < nc ? c : 0;
+    qa[c] = prow_ptr[(size_t)cc * (P + 1) + g];
+    qb[c] = prow_ptr[(size_t)cc * (P + 1) + g + 1];
+  }
+  double v1[NCC];
+#pragma unroll
+  for (int c = 0; c < NCC; ++c) v1[c] = xb[(size_t)(qa[c] < qb[c] ? qa[c] : 0) * K + x];
+  double X = 0.0;
+#pragma unroll
+  for (int c = 0; c < NCC; ++c) {
+    if (c < nc && qa[c] < qb[c]) {
+      X += v1[c];
+      for (int q = qa[c] + 1; q < qb[c]; ++q) X += xb[(size_t)q * K + x];
+    }
+  }
+  return X;
+}
+
+template <int K, bool SUMS>
+__global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
+    double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ xpart,
+    const int* __restrict__ prow_ptr, const double* __restrict__ spart, const int* __restrict__ deg,
+    SpRange spr, int P, int R, long long n_prows, int n_wg_a, int n_gene_wg, double eps,
+    double* __restrict__ nth_out, double* __restrict__ S_out, const double* __restrict__ nth_add,
+    const double* __restrict__ q_part, double* __restrict__ q_out, int n_qwg) {
+  constexpr int K2 = K * K, K3 = K * K * K;
+  constexpr int NCW = (K3 + SKF_CW - 1) / SKF_CW;
+  __shared__ double red[MAX_R * SKF_NPART * SKF_CW];
+  const int tid = threadIdx.x, b = blockIdx.y;
+  const int wgx = blockIdx.x;
+  Stamp st_{};
+  st_.mark(0);
+  if (wgx < n_gene_wg) {
+    const int item = wgx * SKF_NT + tid;
+    if (item >= P * K) return;  // no barrier in this branch
+    const int g = item / K, x = item % K;
+    const double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
+    const double th = theta[((size_t)b * P + g) * K + x];
+    const double ad = nth_add ? nth_add[((size_t)b * P + g) * K + x] : 0.0;
+    const int dg = deg[g];
+    double X = R == 2 ? sk_gene_sum<6>(xb, prow_ptr, P, g, x, K, 6)
+                      : sk_gene_sum<3 * MAX_R>(xb, prow_ptr, P, g, x, K, 3 * R);
+    if (nth_add) X += ad;
+    const size_t o = ((size_t)b * P + g) * K + x;
+    if constexpr (SUMS) nth_out[o] = X;
+    else theta[o] = th * X / (double)dg;
+    return;
+  }
+  if (wgx < n_gene_wg + NCW) {
+    const int cl = tid % SKF_CW, part = tid / SKF_CW;
+    const int cell = (wgx - n_gene_wg) * SKF_CW + cl;
+    const int cc = cell < K3 ? cell : 0;
+    double po[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) po[r] = pr[((size_t)b * R + (r < R ? r : R - 1)) * K3 + cc];
+    for (int r = 0; r < R; ++r) {
+      const int n = spr.hi[r] - spr.lo[r];
+      const int s0 = spr.lo[r] + n * part / SKF_NPART, s1 = spr.lo[r] + n * (part + 1) / SKF_NPART;
+      double S = 0.0;
+      for (int sp = s0; sp < s1; sp += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const double xv = spart[((size_t)b * n_wg_a + (sp + u < s1 ? sp + u : s0)) * K3 + cc];
+          v[u] = sp + u < s1 ? xv : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) S += v[u];
+      }
+      red[(r * SKF_NPART + part) * SKF_CW + cl] = S;
+    }
+    __syncthreads();
+    if (part == 0 && cell < K3) {
+      double npr[MAX_R];
+      double den = eps;
+#pragma unroll
+      for (int r = 0; r < MAX_R; ++r) {
+        if (r < R) {
+          double S = red[(r * SKF_NPART) * SKF_CW + cl];
+#pragma unroll
+          for (int q = 1; q < SKF_NPART; ++q) S += red[(r * SKF_NPART + q) * SKF_CW + cl];
+          if constexpr (SUMS) {
+            S_out[((size_t)b * R + r) * K3 + cell] = S;
+          } else {
+            npr[r] = po[r] * S;
+            den += npr[r];
+          }
+        }
+      }
+      if constexpr (!SUMS) {
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+          if (r < R) pr[((size_t)b * R + r) * K3 + cell] = npr[r] / den;
+      }
+    }
+    return;
+  }
+  // joint model q cells (include/mmsbm_pairs.h): 64 cells of qr per workgroup, 4 threads per cell
+  // each summing a share of the pair launch's S2 partials, combined in order (:1660-1666)
+  {
+    constexpr int NPART = SKF_NT / 64;
+    const int cl = tid & 63, part = tid >> 6;
+    const int cell = (wgx - n_gene_wg - NCW) * 64 + cl;
+    const bool cv = cell < K2;
+    const int cc = cv ? cell : 0;
+    double qo[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) qo[r] = q_out[((size_t)b * R + (r < R ? r : R - 1)) * K2 + cc];
+    const int s0 = n_qwg * part / NPART, s1 = n_qwg * (part + 1) / NPART;
+    for (int r = 0; r < R; ++r) {
+      double S = 0.0;
+      for (int ww = s0; ww < s1; ww += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const double xv = q_part[(((size_t)b * n_qwg + (ww + u < s1 ? ww + u : s0)) * R + r) * K2 + cc];
+          v[u] = ww + u < s1 ? xv : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) S += v[u];
+      }
+      red[(r * NPART + part) * 64 + cl] = S;
+    }
+    __syncthreads();
+    if (part == 0 && cv) {
+      double nq[MAX_R];
+      double den = eps;
+#pragma unroll
+      for (int r = 0; r < MAX_R; ++r) {
+        if (r < R) {
+          double S = red[r * NPART * 64 + cl];
+#pragma unroll
+          for (int q = 1; q < NPART; ++q) S += red[(r * NPART + q) * 64 + cl];
+          nq[r] = qo[r] * S;
+          den += nq[r];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < MAX_R; ++r)
+        if (r < R) q_out[((size_t)b * R + r) * K2 + cell] = nq[r] / den;
+    }
+  }
+}
