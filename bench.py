@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--P", type=int, default=1500)
     ap.add_argument("--E", type=int, default=90000, help="unique triples, train + test")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--hub", default="",
+                    help="FRAC,SHARE: hub-heavy synthetic fold (SHARE of the triples take one gene "
+                         "from the first FRAC of the genes; data.FoldSpec.hub_*), e.g. 0.02,0.3")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl",
@@ -208,11 +211,12 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
                                 pmc[1]["hbm_bytes_per_launch"].get(dom)}}
 
 
-def make_fold(P, E, rank):
+def make_fold(P, E, rank, hub=""):
     from trigenicinteractionpredictor_amd.data import FoldSpec, write_fold
     d = tempfile.mkdtemp(prefix="mmsbm_bench_r%d_" % rank)
     tr, te = os.path.join(d, "train0.dat"), os.path.join(d, "test0.dat")
-    write_fold(FoldSpec(P=P, E=E, seed=7), tr, te)
+    hf, hs = (float(x) for x in hub.split(",")) if hub else (0.0, 0.0)
+    write_fold(FoldSpec(P=P, E=E, seed=7, hub_frac=hf, hub_share=hs), tr, te)
     return tr, te
 
 
@@ -328,7 +332,7 @@ def main():
     if args.launch_check:
         launch_check(args, world, rank)
         return 0
-    train, test = make_fold(args.P, args.E, rank)
+    train, test = make_fold(args.P, args.E, rank, args.hub)
     cpu_rec = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = args.cpu_cores or min(len(os.sched_getaffinity(0)), 16)
@@ -432,6 +436,8 @@ def main():
         roofline = roofline_record(K, host.P, 2, B, E_obs, plan, iter_s, b2b, build_id)
         wl = ("fold0 stand-in" if (args.P, args.E) == (1500, 90000) else
               "synthetic P=%d, E=%d" % (host.P, args.E))
+        if args.hub:
+            wl += " (hub-heavy degrees %s)" % args.hub
         line = {
             "metric": "EM-iterations/sec + final log-likelihood, fold0 K=%d" % K,
             "value": value,

@@ -411,11 +411,11 @@ def test_in_place_link_edit_between_iterations_matches_oracle():
                                rtol=RTOL)
 
 
-@pytest.mark.parametrize("K,env", [(10, {}), (10, {"MMSBM_SK": "0"}), (12, {"MMSBM_SK_WG": "3"}),
-                                   (7, {"MMSBM_SK_WG": "1", "MMSBM_UNITS": "5,9"}), (13, {})])
-def test_kernel_family_and_unit_rounds_match_oracle(tmp_path, monkeypatch, K, env):
+@pytest.mark.parametrize("K,env", [(10, {}), (10, {"MMSBM_SK": "0"}), (12, {"MMSBM_UNITS": "1,1"}),
+                                   (7, {"MMSBM_UNITS": "5,9"}), (13, {})])
+def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
     """K <= 12 runs the small-K kernels (csrc/sk.h), K > 12 the large-K ones; MMSBM_SK=0 forces the
-    large-K family at K=10 and MMSBM_SK_WG forces several unit rounds per workgroup.  Every variant
+    large-K family at K=10, MMSBM_UNITS forces long (16-chunk) or short units.  Every variant
     matches the C oracle (2 iterations, train and held-out likelihood)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)

@@ -53,7 +53,7 @@ def _links(P, E, seed, R=2, hub=0.0, multi=0.05, both=0.03):
     # small-K plans (gcap 0; sp_rows = the workgroup target): stretch-capped units, descriptors
     (300, 5000, (1536, 3072), 0, 1024, 30.0),  # hub genes
     (40, 600, (1, 1), 0, 1024, 0.0),           # one unit per stream: runs split at 32 chunks
-    (200, 6000, (64, 64), 0, 3, 5.0),          # several unit rounds per workgroup
+    (200, 6000, (64, 64), 0, 3, 5.0),          # long units (16 chunks)
     (30, 1500, (1536, 3072), 0, 1024, 0.0),    # more units than chunks
 ])
 def test_plan_invariants(plan_check, P, E, units, gcap, sp_rows, hub):

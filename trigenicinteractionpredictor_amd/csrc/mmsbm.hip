@@ -1413,19 +1413,19 @@ int launch_sk_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const
     if ((rc = lds_opt_in(c, 5, &sk_pass_kernel<K, SK_B>, T::LDS))) return rc;
     sk_pass_kernel<K, SK_B><<<dim3(h.n_wg_b, c->B), NT, T::LDS, s>>>(
         sd.skr[1], sd.sku[1], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, h.n_wg_a,
-        h.sk_L[1], h.rounds_b, c->P, c->R, n_cb, h.n_prows, h.n_wg_b, c->eps);
+        h.sk_L[1], c->P, c->R, n_cb, h.n_prows, h.n_wg_b, c->eps);
   } else if (mode == PASS_A) {
     if (h.n_wg_a == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 4, &sk_pass_kernel<K, SK_A>, T::LDS))) return rc;
     sk_pass_kernel<K, SK_A><<<dim3(h.n_wg_a, c->B), NT, T::LDS, s>>>(
         sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
-        h.sk_L[0], h.rounds_a, c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps);
+        h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps);
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 6, &sk_pass_kernel<K, SK_LL>, T::LDS))) return rc;
     sk_pass_kernel<K, SK_LL><<<dim3(h.n_wg_a, c->B), NT, T::LDS, s>>>(
         sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
-        h.sk_L[0], h.rounds_a, c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps);
+        h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps);
   }
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
@@ -1669,12 +1669,8 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
       units_b = b;
     }
   }
-  // small-K plans: about 1024 workgroups per stream group, units in rounds of NW beyond that;
-  // MMSBM_SK_WG=n lowers the target (tests: several rounds per workgroup)
-  int wg_target = 1024;
-  if (const char* v = getenv("MMSBM_SK_WG")) wg_target = std::max(1, atoi(v));
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
-                           c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, wg_target);
+                           c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk);
   const auto& h = sd.h;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;

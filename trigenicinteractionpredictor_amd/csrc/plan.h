@@ -30,7 +30,7 @@ constexpr int NW = 8;   // waves (units) per workgroup
 // stretches (one wave keeps their V tables and M rows, and contracts them with p at its end) and
 // at most LCAP_SK chunks (its records are staged in the wave's LDS at once).
 constexpr int GU = 4;
-constexpr int LCAP_SK = 32;
+constexpr int LCAP_SK = 16;
 constexpr int UD = 16;  // ints per unit descriptor (below)
 
 struct I4 {
@@ -231,10 +231,9 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   const long long LCAP = small ? LCAP_SK : 64;
   const int lmax_a = (int)std::min(LCAP, std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1)));
   const int lmax_b = (int)std::min(LCAP, std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1)));
-  if (small) {  // unit rounds per workgroup: about wg_target workgroups per stream group
-    const long long ua = (chunks_a + lmax_a - 1) / lmax_a, ub_ = (chunks_b + lmax_b - 1) / lmax_b;
-    pl.rounds_a = (int)std::max<long long>(1, (ua + (long long)NW * wg_target - 1) / ((long long)NW * wg_target));
-    pl.rounds_b = (int)std::max<long long>(1, (ub_ + (long long)NW * wg_target - 1) / ((long long)NW * wg_target));
+  if (small) {  // one unit per wave: rounds stay 1 (wg_target is kept for the plan checker)
+    pl.rounds_a = pl.rounds_b = 1;
+    (void)wg_target;
     pl.wg_ustart.push_back(0);
   }
 

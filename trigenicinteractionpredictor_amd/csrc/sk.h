@@ -26,8 +26,9 @@
 
 enum { SK_A = 0, SK_LL = 1, SK_B = 2 };
 
-constexpr int SKD = 3;                 // chunks of theta gathers in flight ahead of the compute
+constexpr int LC = mmsbm_plan::LCAP_SK;           // most chunks of one unit (gathered at once)
 constexpr int SK_ROWS = 4 * mmsbm_plan::LCAP_SK;  // records staged per wave (one unit)
+constexpr int RPL = (SK_ROWS + 63) / 64;          // staged records per lane
 
 template <int K>
 struct SKT {
@@ -36,13 +37,15 @@ struct SKT {
   static constexpr int NCT = (K2 + 3) / 4;        // 4-cell tiles of a dense K x K row
   static constexpr int NCG = (NCT + 3) / 4;       // groups of 4 cell tiles (one MFMA, 4 blocks)
   static constexpr int SLOT = 4 * NCT;            // doubles per stretch slot (V table, then M row)
-  static constexpr int PSD = (K3 + 1) & ~1;       // staged p_r (16-B aligned)
-  static constexpr int WAVE = mmsbm_plan::GU * SLOT + 2 * SK_ROWS + SK_ROWS;  // slots, records, aux
+  static constexpr int PSD = NCT * 64;            // P^s_r in the X contraction's B-operand layout
+  static constexpr int WAVE = mmsbm_plan::GU * SLOT + 2 * SK_ROWS + SK_ROWS + 64;  // slots, records,
+                                                                                 // aux, transpose
   static constexpr int NS = NG * NCG;             // S accumulators per lane
   static constexpr int LDS = (PSD + NW * WAVE) * 8;
   static_assert(K <= 12, "small-K kernels: K <= 12");
   static_assert(4 * NS * 64 <= PSD + NW * WAVE, "S reduction buffer over the LDS");
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+  static_assert(SLOT >= 4 * NCT, "slot holds a V table / M row");
 };
 
 // p index of P^s[z][cell] (s = the pivot slot z sits in; cell = x K + y over the two other
@@ -57,13 +60,13 @@ struct SkSec {  // workgroup sections of a small-K plan (Plan::sk_wg_end)
 };
 
 // grid (the group's workgroups, B), block 512; group 0 (SK_A, SK_LL) = stream 0, group 1 (SK_B) =
-// streams 1 and 2.  Workgroup w owns unit slots [w rounds NW, (w + 1) rounds NW) (Plan::sk_*).
+// streams 1 and 2.  Wave wv of workgroup w owns unit slot w NW + wv (Plan::sk_*).
 template <int K, int MODE>
 __global__ __launch_bounds__(NT) void sk_pass_kernel(
     const int4* __restrict__ urec, const int* __restrict__ udesc, const int2* __restrict__ urow12,
     const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ cB,
     double* __restrict__ xpart, double* __restrict__ spart, double* __restrict__ partL, SkSec sec,
-    int wg_base, int L, int rounds, int P, int R, long long n_cb, long long n_prows, int n_wg,
+    int wg_base, int L, int P, int R, long long n_cb, long long n_prows, int n_wg,
     double eps) {
   using T = SKT<K>;
   constexpr int NG = T::NG, K2 = T::K2, K3 = T::K3, NCT = T::NCT, NCG = T::NCG, SLOT = T::SLOT;
@@ -73,8 +76,10 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
   const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3, col = lane & 15;
   const int w = blockIdx.x, b = blockIdx.y;
   int sr = 0;  // this workgroup's (stream, rating) section, from the launch arguments alone
-  while (sr + 1 < 3 * R && wg_base + w >= sec.wg_end[sr]) ++sr;
-  const int s = sr / R, r = sr % R;
+#pragma unroll
+  for (int i = 0; i < 3 * MAX_R - 1; ++i)  // (constant indices: the argument array stays in SGPRs)
+    if (i + 1 < 3 * R && wg_base + w >= sec.wg_end[i]) sr = i + 1;
+  const int s = __builtin_amdgcn_readfirstlane(sr / R), r = __builtin_amdgcn_readfirstlane(sr % R);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
   double* Ps = smem;
@@ -82,6 +87,7 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
   double* MSl = wl;                                                 // GU slots: V, then M
   int4* REC = reinterpret_cast<int4*>(wl + mmsbm_plan::GU * SLOT);  // the unit's records
   double* AUX = wl + mmsbm_plan::GU * SLOT + 2 * SK_ROWS;           // row12 (A) / c (B)
+  double* TRl = AUX + SK_ROWS;                                      // Z operand transpose
   double* __restrict__ cBb = cB + (size_t)b * n_cb;
   double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
   Stamp st_{};
@@ -91,24 +97,25 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
   // first round's loads are issued before the p staging below, so they share its round trip.
   struct Unit {
     int nst, d1, d2, d3, c1, prow;
-    int4 rv[2];
-    int2 r12[2];
-    double cv[2];
+    int4 rv[RPL];
+    int2 r12[RPL];
+    double cv[RPL];
     double tv[NG], ts[NG];  // theta_{gene lo}[4 as + hi] (V), theta_{gene hi}[4 at + lo] (S)
+    double pb[NG][NCG];     // B of V: p_r[a = 4 as + hi][cell = 4 (4 cg + blk) + lo]
   };
-  auto load_unit = [&](int rd, Unit& un) {
-    const long long slot = ((long long)w * rounds + rd) * NW + wv;
+  auto load_unit = [&](Unit& un) {
+    const long long slot = (long long)w * NW + wv;
     const int* __restrict__ d = udesc + slot * mmsbm_plan::UD;
-    un.nst = d[5];
-    un.d1 = d[1];
-    un.d2 = d[2];
-    un.d3 = d[3];
-    un.c1 = d[4];
+    un.nst = __builtin_amdgcn_readfirstlane(d[5]);  // wave-uniform (scalar control flow)
+    un.d1 = __builtin_amdgcn_readfirstlane(d[1]);
+    un.d2 = __builtin_amdgcn_readfirstlane(d[2]);
+    un.d3 = __builtin_amdgcn_readfirstlane(d[3]);
+    un.c1 = __builtin_amdgcn_readfirstlane(d[4]);
     un.prow = d[6 + hi];
     const int nrow = 4 * un.c1 > 0 ? 4 * un.c1 : 1;
     const long long rbase = slot * 4 * L;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RPL; ++i) {
       const int idx = lane + 64 * i;
       const long long row = rbase + (idx < nrow ? idx : nrow - 1);
       un.rv[i] = urec[row];
@@ -125,20 +132,47 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
         un.tv[as] = (lo < un.nst && a1 < K) ? v1 : 0.0;
         un.ts[as] = (hi < un.nst && a2 < K) ? v2 : 0.0;
       }
+#pragma unroll
+      for (int as = 0; as < NG; ++as)
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) {
+          const int a = 4 * as + hi, cell = 4 * (4 * cg + blk) + lo;
+          const bool ok = a < K && cell < K2;
+          const double v = p[ok ? a * K2 + cell : 0];
+          un.pb[as][cg] = ok ? v : 0.0;
+        }
     }
   };
   Unit un;
-  load_unit(0, un);
+  load_unit(un);
 
-  // p_r staged once per workgroup (every unit of a workgroup has its rating)
+  // P^s_r staged once per workgroup (every unit of a workgroup has its stream and rating) in the
+  // B-operand layout of the X contraction: PsX[ks][l] = P^s[z][cell] for lane l = (hi, blk, lo),
+  // z = 4 blk + lo, cell = 4 ks + hi (zero outside), so each step of X reads one conflict-free word
   {
-    constexpr int NPI = (K3 + NT - 1) / NT;
+    constexpr int NPI = (T::PSD + NT - 1) / NT;
     double pv[NPI];
 #pragma unroll
-    for (int i = 0; i < NPI; ++i) pv[i] = p[tid + NT * i < K3 ? tid + NT * i : 0];
+    for (int i = 0; i < NPI; ++i) {
+      const int e = tid + NT * i;
+      const int ks = e >> 6, l = e & 63;
+      const int z = 4 * ((l >> 2) & 3) + (l & 3), cell = 4 * ks + (l >> 4);
+      const bool ok = e < T::PSD && ((l >> 2) & 3) < NG && z < K && cell < K2;
+      const int x = ok ? cell / K : 0, y = ok ? cell % K : 0;
+      const double v = p[ok ? sk_pidx<K>(s, z, x, y) : 0];
+      pv[i] = ok ? v : 0.0;
+    }
+    // the unit's records (and row12 / c) into this wave's LDS
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const int idx = lane + 64 * i;
+      REC[idx] = un.rv[i];
+      if constexpr (MODE == SK_A) reinterpret_cast<int2*>(AUX)[idx] = un.r12[i];
+      if constexpr (MODE == SK_B) AUX[idx] = un.cv[i];
+    }
 #pragma unroll
     for (int i = 0; i < NPI; ++i)
-      if (tid + NT * i < K3) Ps[tid + NT * i] = pv[i];
+      if (tid + NT * i < T::PSD) Ps[tid + NT * i] = pv[i];
   }
   __syncthreads();
   st_.mark(6);
@@ -150,28 +184,18 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
     for (int cg = 0; cg < NCG; ++cg) sacc[at][cg] = 0.0;
   double ll = 0.0;
 
-  for (int rd = 0; rd < rounds; ++rd) {
-    if (rd > 0) load_unit(rd, un);
+  if (un.nst > 0) {  // an empty slot only joins the workgroup's barriers
     const int nst = un.nst;
-    if (nst == 0) continue;  // an empty slot (no barrier in the round loop)
     const int c0 = 0, d1 = un.d1, d2 = un.d2, d3 = un.d3, c1 = un.c1;
     st_.t[5] = (unsigned long long)(c1 - c0);
     st_.t[4] = (unsigned long long)nst;
-    auto stretch_end = [&](int t) {  // first chunk after stretch t
-      return t + 1 >= nst ? c1 : t == 0 ? d1 : t == 1 ? d2 : d3;
+    auto stretch_end = [=](int t) {  // first chunk after stretch t (values: no pointer select)
+      int e = c1;
+      if (t + 1 < nst) e = t == 0 ? d1 + 0 : t == 1 ? d2 + 0 : d3 + 0;
+      return e;
     };
-    const double* tv = un.tv;
-    const double* ts = un.ts;
-    const int4* rv = un.rv;
-    const int2* r12 = un.r12;
-    const double* cv = un.cv;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = lane + 64 * i;
-      REC[idx] = rv[i];
-      if constexpr (MODE == SK_A) reinterpret_cast<int2*>(AUX)[idx] = r12[i];
-      if constexpr (MODE == SK_B) AUX[idx] = cv[i];
-    }
+    const auto& tv = un.tv;  // (array references: the indices stay compile-time constants)
+    const auto& ts = un.ts;
     if constexpr (MODE != SK_B) {
       // ---- V_g[cell] = sum_a theta_g[a] p_r[a][cell] for the unit's genes (m = gene, k = a),
       // into slot g of the wave's LDS (cell = b K + h)
@@ -180,44 +204,31 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
         const int cell = 4 * (4 * cg + blk) + lo;
         double v = 0.0;
 #pragma unroll
-        for (int as = 0; as < NG; ++as) {
-          const int a = 4 * as + hi;
-          const bool ok = a < K && cell < K2;
-          const double pv = Ps[ok ? a * K2 + cell : 0];
-          v = mfma4(tv[as], ok ? pv : 0.0, v);
-        }
+        for (int as = 0; as < NG; ++as) v = mfma4(tv[as], un.pb[as][cg], v);
         if (hi < nst && cell < K2) MSl[hi * SLOT + cell] = v;
       }
     }
     wave_lds_sync();
     st_.mark(1);
 
-    // ---- chunk loop.  Stretch t = [d[t], d[t + 1]) (the last ends at c1) uses slot t: its V
-    // table while it runs, its M row once it is done.
+    // ---- chunks.  Stretch t = [d[t], d[t + 1]) (the last ends at c1) uses slot t: its V table
+    // while it runs, its M row once it is done.  Every theta value the unit needs is gathered at
+    // once, straight into the registers of the MFMA operands (lane (obs hi, col): theta_u and
+    // theta_v of its observation, column col; addresses clamped, every load unconditional), so the
+    // unit pays one round trip for all of them; the chunks then run from registers.
     const int4* __restrict__ rec = REC;
-    auto rec_at = [&](int q, int o) { return rec[(q - c0) * 4 + o]; };
-    // theta gathers of one chunk, straight into MFMA operand registers (addresses clamped, every
-    // load unconditional; the values are masked where they are used)
-    struct Ga {
-      double z[NG];  // A: Z: theta_k(obs lo)[4 hs + hi]
-      double a, v;   // M: theta_u(obs hi)[col], theta_v(obs hi)[col]
-    };
     const int colc = col < K ? col : K - 1;
-    auto gather = [&](int q, Ga& g) {
-      const int4 rh = rec_at(q, hi);
-      const int gu = s == 0 ? rh.y : rh.x;          // u slot: j on stream 0, i on streams 1 / 2
-      const int gvv = s == 2 ? rh.y : rh.z;         // v slot: k, except j on stream 2
-      g.a = th[(size_t)gu * K + colc];
-      g.v = th[(size_t)gvv * K + colc];
-      if constexpr (MODE != SK_B) {
-        const int kl = rec_at(q, lo).z;
+    double ga[LC], gv[LC];
 #pragma unroll
-        for (int hs = 0; hs < NG; ++hs) {
-          const int h = 4 * hs + hi;
-          g.z[hs] = th[(size_t)kl * K + (h < K ? h : 0)];
-        }
+    for (int i = 0; i < LC; ++i) {
+      if (i < c1) {  // uniform guard: a short unit issues only its own loads
+        const int4 rh = rec[i * 4 + hi];
+        const int gu = s == 0 ? rh.y : rh.x;   // u slot: j on stream 0, i on streams 1 / 2
+        const int gw = s == 2 ? rh.y : rh.z;   // v slot: k, except j on stream 2
+        ga[i] = th[(unsigned)(gu * K + colc)];
+        gv[i] = th[(unsigned)(gw * K + colc)];
       }
-    };
+    }
     double vb[NG];  // B of Z: V_t[b = col][h = 4 hs + hi]
     auto load_v = [&](int t) {
 #pragma unroll
@@ -232,64 +243,64 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
     int t = 0;
     int send = stretch_end(0);
     if constexpr (MODE != SK_B) load_v(0);
-    constexpr int U = SKD + 1;
-    Ga ring[U];
-#pragma unroll
-    for (int i = 0; i < SKD; ++i) gather(c0 + i < c1 ? c0 + i : c1 - 1, ring[i]);
     const bool kcol = col < K;
-    for (int q0 = c0; q0 < c1; q0 += U) {
 #pragma unroll
-      for (int ph = 0; ph < U; ++ph) {
-        const int q = q0 + ph;
-        if (q >= c1) break;
-        gather(q + SKD < c1 ? q + SKD : c1 - 1, ring[(ph + SKD) % U]);
-        __builtin_amdgcn_sched_barrier(0);  // keep the gathers SKD chunks ahead of their use
-        const Ga& g = ring[ph];
-        const int4 rh = rec_at(q, hi);
-        double c;
-        if constexpr (MODE != SK_B) {
-          // Z[obs hi][b = col] = sum_h theta_k(obs hi)[h] V[b][h]; d = eps + sum_b theta_j[b] Z[b]
-          double z = 0.0;
+    for (int q = 0; q < LC; ++q) {
+      if (q < c1) {  // (a guard, not a break: the loop keeps one exit and unrolls fully)
+      const int4 rh = rec[q * 4 + hi];
+      const double a = kcol ? ga[q] : 0.0;
+      double c;
+      if constexpr (MODE != SK_B) {
+        // theta_k(obs lo)[4 hs + hi], the A operand of Z, is the transpose of the gathered tile
+        // theta_k(obs hi)[col]: through the wave's LDS
+        TRl[lane] = gv[q];
+        wave_lds_sync();
+        double z = 0.0;
 #pragma unroll
-          for (int hs = 0; hs < NG; ++hs) z = mfma4(4 * hs + hi < K ? g.z[hs] : 0.0, vb[hs], z);
-          const double dd = row16_sum((kcol ? g.a : 0.0) * z) + eps;
-          if constexpr (MODE == SK_LL) {
-            if (col == 0) ll += (double)rh.w * log(dd);
-          } else {
-            c = (double)rh.w / dd;
-            if (col == 0) {
-              const int2 rr = reinterpret_cast<const int2*>(AUX)[(q - c0) * 4 + hi];
-              if (rr.x >= 0) {
-                st_wt(cBb + rr.x, c);
-                st_wt(cBb + rr.y, c);
-              }
-            }
-          }
-        } else {
-          c = AUX[(q - c0) * 4 + hi];
+        for (int hs = 0; hs < NG; ++hs) {
+          const int h = 4 * hs + hi;
+          const double x = TRl[16 * lo + h];
+          z = mfma4(h < K ? x : 0.0, vb[hs], z);
         }
-        if constexpr (MODE != SK_LL) {
-          // M += c theta_u (x) theta_v over the chunk's 4 observations (k = observation)
-          m16 = mfma16(kcol ? g.a : 0.0, kcol ? c * g.v : 0.0, m16);
-          if (q + 1 == send) {  // stretch t done: its M row into slot t
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int x = hi + 4 * i;
-              if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
-            }
-            m16 = d4v{0.0, 0.0, 0.0, 0.0};
-            ++t;
-            send = stretch_end(t);
-            if constexpr (MODE == SK_A)
-              if (t < nst) load_v(t);
-          }
+        // Z[obs hi][b = col] = sum_h theta_k(obs hi)[h] V[b][h]; d = eps + sum_b theta_j[b] Z[b]
+        const double dd = row16_sum(a * z) + eps;
+        if constexpr (MODE == SK_LL) {
+          if (col == 0) ll += (double)rh.w * log(dd);
         } else {
-          if (q + 1 == send) {
-            ++t;
-            send = stretch_end(t);
+          c = (double)rh.w / dd;
+          if (col == 0) {
+            const int2 rr = reinterpret_cast<const int2*>(AUX)[q * 4 + hi];
+            if (rr.x >= 0) {
+              st_wt(cBb + rr.x, c);
+              st_wt(cBb + rr.y, c);
+            }
+          }
+        }
+      } else {
+        c = AUX[q * 4 + hi];
+      }
+      if constexpr (MODE != SK_LL) {
+        // M += c theta_u (x) theta_v over the chunk's 4 observations (k = observation)
+        m16 = mfma16(a, kcol ? c * gv[q] : 0.0, m16);
+        if (q + 1 == send) {  // stretch t done: its M row into slot t
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int x = hi + 4 * i;
+            if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
+          }
+          m16 = d4v{0.0, 0.0, 0.0, 0.0};
+          ++t;
+          send = stretch_end(t);
+          if constexpr (MODE == SK_A)
             if (t < nst) load_v(t);
-          }
         }
+      } else {
+        if (q + 1 == send) {
+          ++t;
+          send = stretch_end(t);
+          if (t < nst) load_v(t);
+        }
+      }
       }
     }
     st_.mark(2);
@@ -303,12 +314,9 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
 #pragma unroll
       for (int ks = 0; ks < NCT; ++ks) {
         const int cell = 4 * ks + hi;
-        const bool cok = cell < K2;
-        const double am = MSl[(lo < nst && cok ? lo * SLOT + cell : 0)];
-        const int x = cok ? cell / K : 0, y = cok ? cell % K : 0;
-        const bool pok = blk < NG && z < K && cok;
-        const double bp = Ps[pok ? sk_pidx<K>(s, z, x, y) : 0];
-        xa[ks & 3] = mfma4((lo < nst && cok) ? am : 0.0, pok ? bp : 0.0, xa[ks & 3]);
+        const bool ok = lo < nst && cell < K2;
+        const double am = MSl[ok ? lo * SLOT + cell : 0];
+        xa[ks & 3] = mfma4(ok ? am : 0.0, Ps[ks * 64 + lane], xa[ks & 3]);
       }
       const double xacc = (xa[0] + xa[1]) + (xa[2] + xa[3]);
       if (hi < nst && blk < NG && z < K) st_wt(xb + (size_t)un.prow * K + z, xacc);
@@ -320,12 +328,11 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
           const bool ok = hi < nst && cell < K2;
           const double mb = MSl[ok ? hi * SLOT + cell : 0];
 #pragma unroll
-          for (int at = 0; at < NG; ++at) sacc[at][cg] = mfma4(ts[at], ok ? mb : 0.0, sacc[at][cg]);
+          for (int at = 0; at < NG; ++at) sacc[at][cg] = mfma4(ts[at], ok ? mb : 0.0, 0.0);
         }
       }
       st_.mark(3);
     }
-    wave_lds_sync();  // the next unit overwrites the records and slots
   }
 
   if constexpr (MODE == SK_A) {

@@ -39,6 +39,11 @@ class FoldSpec:
     multi_frac: float = 0.0   # train links given 1..3 extra copies of their line
     both_frac: float = 0.0    # train links given one extra line with the other rating
     dup_frac: float = 0.0     # triples with a repeated gene, e.g. a_a_c
+    # hub-heavy degrees, like the trigenic screens behind get_input (:218-318), where a few query
+    # genes sit in many triples: hub_share of the non-coverage triples take one gene from the
+    # first hub_frac of a gene permutation (0 = uniform, the default)
+    hub_frac: float = 0.0
+    hub_share: float = 0.0
 
 
 # "fold0 stand-in", sized from the LFS byte counts
@@ -67,10 +72,17 @@ def _python_triples(spec: FoldSpec, rng: random.Random):
             seen.add(key)
             cover.append(key)
     rest = []
+    hubs = perm[: max(1, int(P * spec.hub_frac))] if spec.hub_frac else []
     while len(cover) + len(rest) < spec.E:
         if spec.dup_frac and rng.random() < spec.dup_frac:
             a, c = rng.sample(range(P), 2)
             key = tuple(sorted((a, a, c)))
+        elif hubs and rng.random() < spec.hub_share:
+            h = hubs[rng.randrange(len(hubs))]
+            a, c = rng.sample(range(P), 2)
+            if h in (a, c):
+                continue
+            key = tuple(sorted((h, a, c)))
         else:
             key = tuple(sorted(rng.sample(range(P), 3)))
         if key in seen:
