@@ -11,7 +11,7 @@ NAMES = ["passA", "passB", "fin", "spart", "passLL"]
 
 
 def main(path):
-    h = np.fromfile(path, dtype=np.uint64).reshape(5, 1 << 16, 8).astype(np.int64)
+    h = np.fromfile(path, dtype=np.uint64).reshape(5, 1 << 16, 10).astype(np.int64)
     for k, name in enumerate(NAMES):
         t = h[k]
         ok = t[:, 0] != 0
@@ -41,7 +41,12 @@ def main(path):
             print("  chunk loop    %s" % q(t[:, 2] - t[:, 1]))
             print("  epilogue      %s" % q(t[:, 3] - t[:, 2]))
             print("  tail          %s" % q(t[:, 7] - t[:, 3]))
-            print("  wave end      %s" % q(t[:, 7] - t0))
+            # chip-wide timeline from s_memrealtime (100 MHz): when waves start and end relative
+            # to the first wave of the launch, in ns
+            rt0 = t[:, 8].min()
+            print("  start (ns from the first wave) %s" % q((t[:, 8] - rt0) * 10))
+            print("  end   (ns from the first wave) %s" % q((t[:, 9] - rt0) * 10))
+            print("  life  (ns)                     %s" % q((t[:, 9] - t[:, 8]) * 10))
             ch = t[:, 5]
             print("  chunks %s  stretches %s" % (q(ch), q(t[:, 4])))
             if ch.max() > 0 and ch.min() < ch.max():

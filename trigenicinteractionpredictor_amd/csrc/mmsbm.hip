@@ -155,12 +155,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define MMSBM_STAMP 0
 #endif
 __device__ unsigned long long* g_stamp = nullptr;
-constexpr int STAMP_SLOTS = 8;
+constexpr int STAMP_SLOTS = 10;  // 0-7 s_memtime phase marks; 8, 9 s_memrealtime (100 MHz, chip-wide) at 0 and 7
 constexpr long long STAMP_WAVES = 1 << 16;  // per kernel id
 struct Stamp {
   unsigned long long t[STAMP_SLOTS];
   __device__ __forceinline__ void mark(int i) {
-    if constexpr (MMSBM_STAMP) t[i] = __builtin_amdgcn_s_memtime();
+    if constexpr (MMSBM_STAMP) {
+      t[i] = __builtin_amdgcn_s_memtime();
+      if (i == 0) t[8] = __builtin_amdgcn_s_memrealtime();
+      if (i == 7) t[9] = __builtin_amdgcn_s_memrealtime();
+    }
   }
   __device__ __forceinline__ void flush(int kid, long long wave, int lane) {
     if constexpr (MMSBM_STAMP) {
@@ -1410,8 +1414,8 @@ int launch_sk_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const
   int rc;
   if (mode == PASS_B) {
     if (h.n_wg_b == 0) return MMSBM_OK;
-    if ((rc = lds_opt_in(c, 5, &sk_pass_kernel<K, SK_B>, T::LDS))) return rc;
-    sk_pass_kernel<K, SK_B><<<dim3(h.n_wg_b, c->B), NT, T::LDS, s>>>(
+    if ((rc = lds_opt_in(c, 5, &sk_pass_kernel<K, SK_B>, T::LDS_B))) return rc;
+    sk_pass_kernel<K, SK_B><<<dim3(h.n_wg_b, c->B), NT, T::LDS_B, s>>>(
         sd.skr[1], sd.sku[1], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, h.n_wg_a,
         h.sk_L[1], c->P, c->R, n_cb, h.n_prows, h.n_wg_b, c->eps);
   } else if (mode == PASS_A) {

@@ -17,7 +17,10 @@
 //    so pass B reads c coalesced with its records;
 //  * fin sums the X partials per gene (theta update) and the S partials per cell (p update).
 // Bytes per iteration: records + c + X partials (K per partial row) + S partials (K^3 per stream-0
-// workgroup), against K^2 per partial row written and read back by the large-K path.
+// workgroup), against K^2 per partial row written and read back by the large-K path.  These are
+// plain stores: the scattered 8-byte c / X writes as write-through (sc1) stores cost 6-10 us per
+// pass at fold0 (each lane a separate fabric write), the kernel-boundary write-back of the few MB
+// of dirty lines far less (profiles/r03_wt_ab.txt).
 //
 // MFMA lane maps as in mmsbm.hip: v_mfma_f64_4x4x4f64 (lane = 16 hi + 4 blk + lo) takes
 // A[blk][m = lo][k = hi], B[blk][k = hi][n = lo] and gives D[blk][m = hi][n = lo];
@@ -40,6 +43,8 @@ struct SKT {
   static constexpr int PSD = NCT * 64;            // P^s_r in the X contraction's B-operand layout
   static constexpr int WAVE = mmsbm_plan::GU * SLOT + 2 * SK_ROWS + SK_ROWS + 64;  // slots, records,
                                                                                  // aux, transpose
+  static constexpr int WAVE_B = WAVE - 64;        // pass B: no Z transpose
+  static constexpr int LDS_B = (PSD + NW * WAVE_B) * 8;
   static constexpr int NS = NG * NCG;             // S accumulators per lane
   static constexpr int LDS = (PSD + NW * WAVE) * 8;
   static_assert(K <= 12, "small-K kernels: K <= 12");
@@ -47,6 +52,17 @@ struct SKT {
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
   static_assert(SLOT >= 4 * NCT, "slot holds a V table / M row");
 };
+
+// n / d by v_rcp_f64 and two Newton steps plus a residual correction (within an ulp or two of the
+// IEEE quotient; d > 0 here): a shorter dependent chain than the IEEE division's scale / fixup
+// sequence in the chunk loop.  Deterministic, so results stay bitwise reproducible.
+__device__ __forceinline__ double sk_div(double n, double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(fma(-d, r, 1.0), r, r);
+  r = fma(fma(-d, r, 1.0), r, r);
+  const double q = n * r;
+  return fma(fma(-d, q, n), r, q);
+}
 
 // p index of P^s[z][cell] (s = the pivot slot z sits in; cell = x K + y over the two other
 // slots u, v in order): s = 0 p[z][x][y], s = 1 p[x][z][y], s = 2 p[x][y][z]
@@ -83,7 +99,7 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
   double* Ps = smem;
-  double* wl = smem + T::PSD + wv * T::WAVE;
+  double* wl = smem + T::PSD + wv * (MODE == SK_B ? T::WAVE_B : T::WAVE);
   double* MSl = wl;                                                 // GU slots: V, then M
   int4* REC = reinterpret_cast<int4*>(wl + mmsbm_plan::GU * SLOT);  // the unit's records
   double* AUX = wl + mmsbm_plan::GU * SLOT + 2 * SK_ROWS;           // row12 (A) / c (B)
@@ -92,6 +108,9 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
   double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
   Stamp st_{};
   st_.mark(0);
+#ifdef MMSBM_SK_EXIT  // measurement builds: leave after phase MMSBM_SK_EXIT (0 = at once)
+  if (MMSBM_SK_EXIT == 0 && b >= 0) return;
+#endif
 
   // One slot's descriptor, records (+ row12 / c) and pivot-gene theta, loaded together.  The
   // first round's loads are issued before the p staging below, so they share its round trip.
@@ -176,6 +195,9 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
   }
   __syncthreads();
   st_.mark(6);
+#ifdef MMSBM_SK_EXIT
+  if (MMSBM_SK_EXIT == 1 && b >= 0) return;
+#endif
 
   double sacc[NG][NCG];  // SK_A: this wave's share of S_r[a][cell], a = 4 at + hi
 #pragma unroll
@@ -267,12 +289,12 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
         if constexpr (MODE == SK_LL) {
           if (col == 0) ll += (double)rh.w * log(dd);
         } else {
-          c = (double)rh.w / dd;
+          c = sk_div((double)rh.w, dd);
           if (col == 0) {
             const int2 rr = reinterpret_cast<const int2*>(AUX)[q * 4 + hi];
             if (rr.x >= 0) {
-              st_wt(cBb + rr.x, c);
-              st_wt(cBb + rr.y, c);
+              cBb[rr.x] = c;
+              cBb[rr.y] = c;
             }
           }
         }
@@ -319,7 +341,7 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
         xa[ks & 3] = mfma4(ok ? am : 0.0, Ps[ks * 64 + lane], xa[ks & 3]);
       }
       const double xacc = (xa[0] + xa[1]) + (xa[2] + xa[3]);
-      if (hi < nst && blk < NG && z < K) st_wt(xb + (size_t)un.prow * K + z, xacc);
+      if (hi < nst && blk < NG && z < K) xb[(size_t)un.prow * K + z] = xacc;
       if constexpr (MODE == SK_A) {
         // ---- S_r[a][cell] += sum_q theta_{g_q}[a] M_q[cell] (m = a, k = q, n = cell)
 #pragma unroll
@@ -370,7 +392,7 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
 #pragma unroll
         for (int cg = 0; cg < NCG; ++cg) {
           const int a = 4 * at + hi, cell = 4 * (4 * cg + blk) + lo;
-          if (a < K && cell < K2) st_wt(out + a * K2 + cell, sacc[at][cg]);
+          if (a < K && cell < K2) out[a * K2 + cell] = sacc[at][cg];
         }
     }
   }
