@@ -104,7 +104,10 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
       for (int i = 0; i < 4 * d[4]; ++i) {
         const I4& a = pl.sk_urec[g][(size_t)slot * 4 * L + i];
         const I4& b = pl.rows[4LL * du[0] + i];
-        if (a.x != b.x || a.y != b.y || a.z != b.z || a.w != b.w) return fail("slot record", slot, i);
+        // group 1 (streams 1, 2) carries the observation's count n = its stream-0 row's w (0: padding)
+        const int bw = g == 0 ? b.w : (b.w < pl.n_rows0 ? pl.rows[b.w].w : 0);
+        if (a.x != b.x || a.y != b.y || a.z != b.z || a.w != bw) return fail("slot record", slot, i);
+        if (g == 1 && b.w < pl.n_rows0 && bw <= 0) return fail("slot count", slot, i);
       }
     }
   }
@@ -143,9 +146,18 @@ int main() {
     for (int r = 0; r < R; ++r)
       if (scanf("%d", &counts[e * R + r]) != 1) return fail("counts");
   }
-  const bool small = gcap == 0;  // gcap 0: the small-K plan of sk.h (sp_rows = its wg_target)
-  const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows)
+  // gcap 0: the small-K plan of sk.h (sp_rows = its wg_target); -1: the same, fill-packed (fused launch)
+  const bool small = gcap <= 0, fill = gcap < 0;
+  const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill)
                         : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows);
+  if (fill) {  // every unit but the last of its (stream, rating) section is full: LCAP_SK chunks or GU stretches
+    for (long long u = 0; u + 1 < pl.n_units; ++u) {
+      const int* d = &pl.udesc[(size_t)u * UD];
+      const int* dn = &pl.udesc[(size_t)(u + 1) * UD];
+      if (dn[14] != d[14]) continue;  // the section's last unit
+      if (d[4] - d[0] != LCAP_SK && d[5] != GU) return fail("fill", (int)u, d[4] - d[0]);
+    }
+  }
 
   // 1. every observation appears once per stream, with its count on stream 0 and its stream-0
   //    row on streams 1 / 2; padding rows carry a zero count / the zero c slot

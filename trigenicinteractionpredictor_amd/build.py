@@ -22,7 +22,8 @@ SRC_IO = os.path.join(PKG, "csrc", "fold_io.cpp")
 LIB_IO = os.path.join(OUT_DIR, "libmmsbm_io.so")  # host-only ingestion (include/mmsbm_io.h)
 ARCH = os.environ.get("MMSBM_OFFLOAD_ARCH", "gfx950")
 DEPS = {
-    SRC: [os.path.join(PKG, "csrc", "plan.h"), os.path.join(INCLUDE, "mmsbm.h")],
+    SRC: [os.path.join(PKG, "csrc", "plan.h"), os.path.join(PKG, "csrc", "sk.h"),
+          os.path.join(INCLUDE, "mmsbm.h")],
     SRC_PAIRS: [os.path.join(INCLUDE, "mmsbm.h"), os.path.join(INCLUDE, "mmsbm_pairs.h")],
 }
 

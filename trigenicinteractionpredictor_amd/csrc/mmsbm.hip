@@ -1208,6 +1208,7 @@ struct mmsbm_ctx {
   double eps = 1e-10;
   int gcap = 0;                  // most pivot genes per stream-0 workgroup (<= KT<K>::GMAX)
   bool sk = false;               // K <= 12: the small-K kernels of sk.h (MMSBM_SK=0: the large-K ones)
+  bool sk_fused = false;         // small-K: one fused E-step launch (SK_U) instead of pass A + pass B
   SetDev sets[2];
   int* deg = nullptr;            // device, owned
   std::vector<int> deg_host;
@@ -1413,23 +1414,29 @@ int launch_sk_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const
   const int2* r12 = reinterpret_cast<const int2*>(sd.skrow12);
   int rc;
   if (mode == PASS_B) {
-    if (h.n_wg_b == 0) return MMSBM_OK;
+    if (h.n_wg_b == 0 || c->sk_fused) return MMSBM_OK;  // fused: streams 1, 2 ran in "pass A"
     if ((rc = lds_opt_in(c, 5, &sk_pass_kernel<K, SK_B>, T::LDS_B))) return rc;
     sk_pass_kernel<K, SK_B><<<dim3(h.n_wg_b, c->B), NT, T::LDS_B, s>>>(
         sd.skr[1], sd.sku[1], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, h.n_wg_a,
-        h.sk_L[1], c->P, c->R, n_cb, h.n_prows, h.n_wg_b, c->eps);
+        h.sk_L[1], c->P, c->R, n_cb, h.n_prows, h.n_wg_b, c->eps, nullptr, nullptr, 0);
+  } else if (mode == PASS_A && c->sk_fused) {  // the fused E-step: every stream in one launch
+    if (h.n_wg_a + h.n_wg_b == 0) return MMSBM_OK;
+    if ((rc = lds_opt_in(c, 7, &sk_pass_kernel<K, SK_U>, T::LDS_U))) return rc;
+    sk_pass_kernel<K, SK_U><<<dim3(h.n_wg_a + h.n_wg_b, c->B), NT, T::LDS_U, s>>>(
+        sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
+        h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps, sd.skr[1], sd.sku[1], h.sk_L[1]);
   } else if (mode == PASS_A) {
     if (h.n_wg_a == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 4, &sk_pass_kernel<K, SK_A>, T::LDS))) return rc;
     sk_pass_kernel<K, SK_A><<<dim3(h.n_wg_a, c->B), NT, T::LDS, s>>>(
         sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
-        h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps);
+        h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps, nullptr, nullptr, 0);
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 6, &sk_pass_kernel<K, SK_LL>, T::LDS))) return rc;
     sk_pass_kernel<K, SK_LL><<<dim3(h.n_wg_a, c->B), NT, T::LDS, s>>>(
         sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
-        h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps);
+        h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps, nullptr, nullptr, 0);
   }
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
@@ -1631,6 +1638,8 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
       c->ws_bytes = 0;
     }
     c->sk = sk;
+    const char* f = getenv("MMSBM_SK_FUSED");  // the fused E-step (SK_U); 0: pass A + pass B
+    c->sk_fused = sk && !(f && f[0] == '0');
   }
   ++c->gen;
   c->attr = 0;      // the dynamic-LDS opt-ins are per kernel, and the kernels depend on K
@@ -1664,8 +1673,9 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   sd.release();
   const bool em = which == MMSBM_SET_TRAIN;
   // unit counts do not depend on B, so a sample's sums (and its bits) are the same whatever its
-  // batch; MMSBM_UNITS="a,b" overrides them (tests: tiny units force every split path)
-  int units_a = 1536, units_b = 3072;
+  // batch; MMSBM_UNITS="a,b" overrides them (tests: tiny units force every split path).  The fused
+  // small-K launch packs full units (as few as the chunk cap allows: the grid must be resident).
+  int units_a = c->sk_fused ? 1 : 1536, units_b = c->sk_fused ? 1 : 3072;
   if (const char* u = getenv("MMSBM_UNITS")) {
     int a = 0, b = 0;
     if (sscanf(u, "%d,%d", &a, &b) == 2 && a > 0 && b > 0) {
@@ -1674,7 +1684,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
     }
   }
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
-                           c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk);
+                           c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, 1024, c->sk_fused);
   const auto& h = sd.h;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;

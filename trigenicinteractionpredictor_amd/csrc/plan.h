@@ -84,14 +84,18 @@ struct Plan {
 };
 
 // Greedy unit packing over the runs of one (stream, rating): a unit takes whole runs while they
-// fit in `lmax` chunks (and, on stream 0, `gcap` genes), a run longer than `lmax` is split.
+// fit in `lmax` chunks (and, on stream 0, `gcap` genes), a run longer than `lmax` is split.  With
+// `fill`, a run that does not fit is split at the unit's end instead, so every unit but the last of
+// a section holds exactly `lmax` chunks unless it reached `gcap` genes first (the fused small-K
+// launch: fewest units, so the whole grid is resident at once).
 // Returns unit boundaries (chunk offsets relative to the stream section).
-inline void pack_units(const std::vector<int>& run_chunks, int lmax, int gcap, std::vector<int>& ub) {
+inline void pack_units(const std::vector<int>& run_chunks, int lmax, int gcap, std::vector<int>& ub,
+                       bool fill = false) {
   ub.clear();
   ub.push_back(0);
   int cur = 0, genes = 0, pos = 0;
   for (int nch : run_chunks) {
-    if (cur > 0 && (cur + nch > lmax || genes + 1 > gcap)) {
+    if (cur > 0 && (genes + 1 > gcap || cur >= lmax || (!fill && cur + nch > lmax))) {
       ub.push_back(pos);
       cur = 0;
       genes = 0;
@@ -157,6 +161,9 @@ inline void make_slots(Plan& pl) {
         for (long long i = 0; i < 4LL * L; ++i) {
           const long long row = row0 + (i < nrow ? i : nrow - 1);  // padding: the unit's last row
           rec[i] = pl.rows[row];
+          // streams 1, 2: the observation's count n (its stream-0 row's w; 0 on padding rows), for
+          // the fused kernel that computes c itself (pass B reads c by position and ignores w)
+          if (g == 1) rec[i].w = rec[i].w < pl.n_rows0 ? pl.rows[rec[i].w].w : 0;
           if (i < nrow) pos[row] = slot * 4 * L + i;
         }
       }
@@ -180,7 +187,7 @@ inline void make_slots(Plan& pl) {
 // K^3 partial, so large K wants more rows per partial).
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
-                  int wg_target = 1024) {
+                  int wg_target = 1024, bool fill = false) {
   Plan pl;
   pl.R = R;
   pl.P = P;
@@ -269,7 +276,8 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       }
       // units
       std::vector<int> ub;
-      pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? GU : s == 0 ? gcap : (1 << 30), ub);
+      pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? GU : s == 0 ? gcap : (1 << 30), ub,
+                 small && fill);
       const int nunits = (int)ub.size() - 1;
       // chunk -> gene
       const int nch = ub.empty() ? 0 : ub.back();

@@ -27,7 +27,11 @@
 // v_mfma_f64_16x16x4f64 takes A[m = l & 15][k = l >> 4], B[k = l >> 4][n = l & 15] and gives
 // D[m = (l >> 4) + 4 i][n = l & 15] in element i.
 
-enum { SK_A = 0, SK_LL = 1, SK_B = 2 };
+// SK_U (the fused E-step): every stream in ONE launch, each observation's d (and c = n / d) computed
+// by the wave of every stream it sits in (stream s contracts V^s_g, the lattice with the pivot slot
+// s summed against theta_g), so nothing waits for another workgroup: pass A's c stores, pass B's c
+// loads and one dependent launch per iteration go away for 2x the Z / d / c work.
+enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
 
 constexpr int LC = mmsbm_plan::LCAP_SK;           // most chunks of one unit (gathered at once)
 constexpr int SK_ROWS = 4 * mmsbm_plan::LCAP_SK;  // records staged per wave (one unit)
@@ -40,17 +44,27 @@ struct SKT {
   static constexpr int NCT = (K2 + 3) / 4;        // 4-cell tiles of a dense K x K row
   static constexpr int NCG = (NCT + 3) / 4;       // groups of 4 cell tiles (one MFMA, 4 blocks)
   static constexpr int SLOT = 4 * NCT;            // doubles per stretch slot (V table, then M row)
-  static constexpr int PSD = NCT * 64;            // P^s_r in the X contraction's B-operand layout
-  static constexpr int WAVE = mmsbm_plan::GU * SLOT + 2 * SK_ROWS + SK_ROWS + 64;  // slots, records,
-                                                                                 // aux, transpose
-  static constexpr int WAVE_B = WAVE - 64;        // pass B: no Z transpose
+  // P^s_r staged per workgroup, plain [z][cell] order, zero past K^3 up to the last word the
+  // unguarded V-operand reads touch (rows a >= K of the 4-wide a tiles, cells up to 16 NCG)
+  static constexpr int PVR = (4 * NG - 1) * K2 + 16 * NCG;
+  static constexpr int PSD = ((PVR > K3 ? PVR : K3) + 1) & ~1;
+  static constexpr int WAVE = mmsbm_plan::GU * SLOT + 2 * SK_ROWS + SK_ROWS + 64 + SK_ROWS;  // slots,
+                                                             // records, aux, transpose, d / c words
+  static constexpr int WAVE_B = WAVE - 64 - SK_ROWS;  // pass B: c arrives in aux
   static constexpr int LDS_B = (PSD + NW * WAVE_B) * 8;
+  static constexpr int WAVE_U = WAVE - SK_ROWS;   // fused: no row12 / c staging
+  static constexpr int NPV = (PSD + NT - 1) / NT; // staged words per thread
+  static constexpr int LDS_U = (PSD + NW * WAVE_U) * 8;
   static constexpr int NS = NG * NCG;             // S accumulators per lane
   static constexpr int LDS = (PSD + NW * WAVE) * 8;
   static_assert(K <= 12, "small-K kernels: K <= 12");
-  static_assert(4 * NS * 64 <= PSD + NW * WAVE, "S reduction buffer over the LDS");
+  static_assert(4 * NS * 64 <= PSD + NW * WAVE_U, "S reduction buffer over the LDS");
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
   static_assert(SLOT >= 4 * NCT, "slot holds a V table / M row");
+  // the unguarded V / M reads stay inside the slots and the records (finite words)
+  static_assert((mmsbm_plan::GU - 1) * SLOT + 15 * K + 4 * NG <= mmsbm_plan::GU * SLOT + 2 * SK_ROWS,
+                "V reads past the wave's slots and records");
+  static_assert(16 * NCG <= SLOT + 2 * SK_ROWS, "S operand reads past the slots and records");
 };
 
 // n / d by v_rcp_f64 and two Newton steps plus a residual correction (within an ulp or two of the
@@ -76,34 +90,44 @@ struct SkSec {  // workgroup sections of a small-K plan (Plan::sk_wg_end)
 };
 
 // grid (the group's workgroups, B), block 512; group 0 (SK_A, SK_LL) = stream 0, group 1 (SK_B) =
-// streams 1 and 2.  Wave wv of workgroup w owns unit slot w NW + wv (Plan::sk_*).
+// streams 1 and 2; SK_U: both groups, group 0's n_wg workgroups first, then group 1's (urec1,
+// udesc1, L1).  Wave wv of workgroup w of a group owns unit slot w NW + wv (Plan::sk_*).
 template <int K, int MODE>
-__global__ __launch_bounds__(NT) void sk_pass_kernel(
+// (pass B: 6 waves per SIMD = three workgroups per CU, which its LDS allows)
+__global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
     const int4* __restrict__ urec, const int* __restrict__ udesc, const int2* __restrict__ urow12,
     const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ cB,
     double* __restrict__ xpart, double* __restrict__ spart, double* __restrict__ partL, SkSec sec,
     int wg_base, int L, int P, int R, long long n_cb, long long n_prows, int n_wg,
-    double eps) {
+    double eps, const int4* __restrict__ urec1, const int* __restrict__ udesc1, int L1) {
   using T = SKT<K>;
   constexpr int NG = T::NG, K2 = T::K2, K3 = T::K3, NCT = T::NCT, NCG = T::NCG, SLOT = T::SLOT;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3, col = lane & 15;
-  const int w = blockIdx.x, b = blockIdx.y;
+  const int wx = blockIdx.x, b = blockIdx.y;
+  const bool g1 = MODE == SK_U && wx >= n_wg;  // SK_U: a group-1 (stream 1 / 2) workgroup
+  const int w = g1 ? wx - n_wg : wx;            // workgroup within its group
+  if (g1) {
+    urec = urec1;
+    udesc = udesc1;
+    L = L1;
+  }
   int sr = 0;  // this workgroup's (stream, rating) section, from the launch arguments alone
 #pragma unroll
   for (int i = 0; i < 3 * MAX_R - 1; ++i)  // (constant indices: the argument array stays in SGPRs)
-    if (i + 1 < 3 * R && wg_base + w >= sec.wg_end[i]) sr = i + 1;
+    if (i + 1 < 3 * R && wg_base + wx >= sec.wg_end[i]) sr = i + 1;
   const int s = __builtin_amdgcn_readfirstlane(sr / R), r = __builtin_amdgcn_readfirstlane(sr % R);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-  double* Ps = smem;
-  double* wl = smem + T::PSD + wv * (MODE == SK_B ? T::WAVE_B : T::WAVE);
+  double* PV = smem;  // P^s_r[z][cell] (cell = x K + y over the u, v slots), zero past K^3
+  double* wl = smem + T::PSD + wv * (MODE == SK_B ? T::WAVE_B : MODE == SK_U ? T::WAVE_U : T::WAVE);
   double* MSl = wl;                                                 // GU slots: V, then M
   int4* REC = reinterpret_cast<int4*>(wl + mmsbm_plan::GU * SLOT);  // the unit's records
   double* AUX = wl + mmsbm_plan::GU * SLOT + 2 * SK_ROWS;           // row12 (A) / c (B)
-  double* TRl = AUX + SK_ROWS;                                      // Z operand transpose
+  double* TRl = MODE == SK_U ? AUX : AUX + SK_ROWS;                 // Z operand transpose
+  double* DL = TRl + 64;                                            // d, then c, per observation
   double* __restrict__ cBb = cB + (size_t)b * n_cb;
   double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
   Stamp st_{};
@@ -112,15 +136,25 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
   if (MMSBM_SK_EXIT == 0 && b >= 0) return;
 #endif
 
-  // One slot's descriptor, records (+ row12 / c) and pivot-gene theta, loaded together.  The
-  // first round's loads are issued before the p staging below, so they share its round trip.
+  // P^s_r once per workgroup (every unit of a workgroup has its stream and rating): its loads go
+  // out first, so the barrier that publishes it (before the V tables) waits about one round trip.
+  double pvv[T::NPV];
+#pragma unroll
+  for (int i = 0; i < T::NPV; ++i) {
+    const int e = tid + NT * i;
+    const bool ok = e < K3;
+    const int z = ok ? e / K2 : 0, x = ok ? (e % K2) / K : 0, y = ok ? e % K : 0;
+    const double v = p[ok ? sk_pidx<K>(s, z, x, y) : 0];
+    pvv[i] = ok ? v : 0.0;
+  }
+
+  // One slot's descriptor, records (+ row12 / c) and pivot-gene theta, loaded together.
   struct Unit {
     int nst, d1, d2, d3, c1, prow;
     int4 rv[RPL];
     int2 r12[RPL];
     double cv[RPL];
     double tv[NG], ts[NG];  // theta_{gene lo}[4 as + hi] (V), theta_{gene hi}[4 at + lo] (S)
-    double pb[NG][NCG];     // B of V: p_r[a = 4 as + hi][cell = 4 (4 cg + blk) + lo]
   };
   auto load_unit = [&](Unit& un) {
     const long long slot = (long long)w * NW + wv;
@@ -131,7 +165,8 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
     un.d3 = __builtin_amdgcn_readfirstlane(d[3]);
     un.c1 = __builtin_amdgcn_readfirstlane(d[4]);
     un.prow = d[6 + hi];
-    const int nrow = 4 * un.c1 > 0 ? 4 * un.c1 : 1;
+    const int nrow = 4 * L;  // the slot's capacity (every row valid: make_slots pads), so the record
+                             // loads do not wait for the descriptor
     const long long rbase = slot * 4 * L;
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
@@ -151,49 +186,26 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
         un.tv[as] = (lo < un.nst && a1 < K) ? v1 : 0.0;
         un.ts[as] = (hi < un.nst && a2 < K) ? v2 : 0.0;
       }
-#pragma unroll
-      for (int as = 0; as < NG; ++as)
-#pragma unroll
-        for (int cg = 0; cg < NCG; ++cg) {
-          const int a = 4 * as + hi, cell = 4 * (4 * cg + blk) + lo;
-          const bool ok = a < K && cell < K2;
-          const double v = p[ok ? a * K2 + cell : 0];
-          un.pb[as][cg] = ok ? v : 0.0;
-        }
     }
   };
   Unit un;
   load_unit(un);
 
-  // P^s_r staged once per workgroup (every unit of a workgroup has its stream and rating) in the
-  // B-operand layout of the X contraction: PsX[ks][l] = P^s[z][cell] for lane l = (hi, blk, lo),
-  // z = 4 blk + lo, cell = 4 ks + hi (zero outside), so each step of X reads one conflict-free word
-  {
-    constexpr int NPI = (T::PSD + NT - 1) / NT;
-    double pv[NPI];
 #pragma unroll
-    for (int i = 0; i < NPI; ++i) {
-      const int e = tid + NT * i;
-      const int ks = e >> 6, l = e & 63;
-      const int z = 4 * ((l >> 2) & 3) + (l & 3), cell = 4 * ks + (l >> 4);
-      const bool ok = e < T::PSD && ((l >> 2) & 3) < NG && z < K && cell < K2;
-      const int x = ok ? cell / K : 0, y = ok ? cell % K : 0;
-      const double v = p[ok ? sk_pidx<K>(s, z, x, y) : 0];
-      pv[i] = ok ? v : 0.0;
-    }
-    // the unit's records (and row12 / c) into this wave's LDS
+  for (int i = 0; i < T::NPV; ++i)
+    if (tid + NT * i < T::PSD) PV[tid + NT * i] = pvv[i];
+  // the unit's records (and row12 / c) into this wave's LDS
 #pragma unroll
-    for (int i = 0; i < RPL; ++i) {
-      const int idx = lane + 64 * i;
-      REC[idx] = un.rv[i];
-      if constexpr (MODE == SK_A) reinterpret_cast<int2*>(AUX)[idx] = un.r12[i];
-      if constexpr (MODE == SK_B) AUX[idx] = un.cv[i];
-    }
-#pragma unroll
-    for (int i = 0; i < NPI; ++i)
-      if (tid + NT * i < T::PSD) Ps[tid + NT * i] = pv[i];
+  for (int i = 0; i < RPL; ++i) {
+    const int idx = lane + 64 * i;
+    REC[idx] = un.rv[i];
+    if constexpr (MODE == SK_A) reinterpret_cast<int2*>(AUX)[idx] = un.r12[i];
+    if constexpr (MODE == SK_B) AUX[idx] = un.cv[i];
   }
-  __syncthreads();
+  // pass B reads P^s only in the X contraction, behind the barrier after its chunk loop; the
+  // passes that form V tables publish it here
+  if constexpr (MODE == SK_B) wave_lds_sync();
+  else __syncthreads();
   st_.mark(6);
 #ifdef MMSBM_SK_EXIT
   if (MMSBM_SK_EXIT == 1 && b >= 0) return;
@@ -216,184 +228,195 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
       if (t + 1 < nst) e = t == 0 ? d1 + 0 : t == 1 ? d2 + 0 : d3 + 0;
       return e;
     };
+    // ---- theta gathers.  Every theta value the unit needs is gathered at once, straight into the
+    // registers of the MFMA operands (lane (obs hi, col): theta_u and theta_v of its observation,
+    // column col), before the V tables are formed, so the round trip overlaps that work.  Columns
+    // col >= K are zeroed where a product needs it (the Z operand and d), at their first use, so no
+    // select waits for a load here.
+    const int4* __restrict__ rec = REC;
+    const int colc = col < K ? col : K - 1;
+    const bool kcol = col < K;
+    const double km = kcol ? 1.0 : 0.0;
+    double ga[LC], gv[LC];
+    auto gather = [&](int i) {
+      ga[i] = 0.0;  // (chunks past the unit's end stay zero)
+      gv[i] = 0.0;
+      if (i < c1) {  // uniform guard: a short unit issues only its own loads
+        const int4 rh = rec[i * 4 + hi];
+        const int gu = s == 0 ? rh.y : rh.x;   // u slot: j on stream 0, i on streams 1 / 2
+        const int gw = s == 2 ? rh.y : rh.z;   // v slot: k, except j on stream 2
+        ga[i] = th[(unsigned)(gu * K + colc)];  // (col >= K: a finite copy of column K - 1)
+        gv[i] = th[(unsigned)(gw * K + colc)];
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < LC; ++i) gather(i);
     const auto& tv = un.tv;  // (array references: the indices stay compile-time constants)
-    const auto& ts = un.ts;
     if constexpr (MODE != SK_B) {
-      // ---- V_g[cell] = sum_a theta_g[a] p_r[a][cell] for the unit's genes (m = gene, k = a),
-      // into slot g of the wave's LDS (cell = b K + h)
+      // ---- V_g[cell] = sum_a theta_g[a] P^s[a][cell] for the unit's genes (m = gene, k = a, B
+      // from the staged lattice: rows a >= K meet zero theta, words past K^3 are zero), into slot g
+      // of the wave's LDS (cell = b K + h).  Every word of the GU slots is written (zero past K^2
+      // and for absent stretches), so the unguarded V / M reads below see finite values.
 #pragma unroll
       for (int cg = 0; cg < NCG; ++cg) {
         const int cell = 4 * (4 * cg + blk) + lo;
         double v = 0.0;
 #pragma unroll
-        for (int as = 0; as < NG; ++as) v = mfma4(tv[as], un.pb[as][cg], v);
-        if (hi < nst && cell < K2) MSl[hi * SLOT + cell] = v;
+        for (int as = 0; as < NG; ++as) v = mfma4(tv[as], PV[(4 * as + hi) * K2 + cell], v);
+        if (cell < SLOT) MSl[hi * SLOT + cell] = cell < K2 ? v : 0.0;
       }
+    } else {
+      // pass B forms no V tables: the slots' words past each M row stay finite (zero)
+#pragma unroll
+      for (int i = 0; i < (mmsbm_plan::GU * SLOT + 63) / 64; ++i)
+        if (lane + 64 * i < mmsbm_plan::GU * SLOT) MSl[lane + 64 * i] = 0.0;
     }
     wave_lds_sync();
     st_.mark(1);
 
-    // ---- chunks.  Stretch t = [d[t], d[t + 1]) (the last ends at c1) uses slot t: its V table
-    // while it runs, its M row once it is done.  Every theta value the unit needs is gathered at
-    // once, straight into the registers of the MFMA operands (lane (obs hi, col): theta_u and
-    // theta_v of its observation, column col; addresses clamped, every load unconditional), so the
-    // unit pays one round trip for all of them; the chunks then run from registers.
-    const int4* __restrict__ rec = REC;
-    const int colc = col < K ? col : K - 1;
-    double ga[LC], gv[LC];
+    if constexpr (MODE != SK_B) {
+      // ---- d of every observation of the unit.  Per chunk: Z[obs hi][b = col] =
+      // sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA (A = theta_v(obs lo)[4 hs + hi], the transpose of
+      // the gathered tile, through the wave's LDS), d = eps + sum_b theta_u[b] Z[b] by a DPP row sum;
+      // d is parked at DL[4 q + obs] (one word per observation = per lane of the wave).
+      double vb[NG];  // B of Z: V_t[b = col][h = 4 hs + hi] (unguarded: zero A columns cancel h >= K)
+      auto load_v = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < LC; ++i) {
-      if (i < c1) {  // uniform guard: a short unit issues only its own loads
-        const int4 rh = rec[i * 4 + hi];
-        const int gu = s == 0 ? rh.y : rh.x;   // u slot: j on stream 0, i on streams 1 / 2
-        const int gw = s == 2 ? rh.y : rh.z;   // v slot: k, except j on stream 2
-        ga[i] = th[(unsigned)(gu * K + colc)];
-        gv[i] = th[(unsigned)(gw * K + colc)];
-      }
-    }
-    double vb[NG];  // B of Z: V_t[b = col][h = 4 hs + hi]
-    auto load_v = [&](int t) {
+        for (int hs = 0; hs < NG; ++hs) vb[hs] = MSl[t * SLOT + col * K + 4 * hs + hi];
+      };
+      int t = 0;
+      int send = stretch_end(0);
+      load_v(0);
 #pragma unroll
-      for (int hs = 0; hs < NG; ++hs) {
-        const int h = 4 * hs + hi;
-        const bool ok = col < K && h < K;
-        const double x = MSl[t * SLOT + (ok ? col * K + h : 0)];
-        vb[hs] = ok ? x : 0.0;
-      }
-    };
-    d4v m16 = d4v{0.0, 0.0, 0.0, 0.0};
-    int t = 0;
-    int send = stretch_end(0);
-    if constexpr (MODE != SK_B) load_v(0);
-    const bool kcol = col < K;
+      for (int q = 0; q < LC; ++q) {
+        if (q < c1) {  // (a guard, not a break: the loop keeps one exit and unrolls fully)
+          TRl[lane] = gv[q] * km;
+          wave_lds_sync();
+          double z = 0.0;
 #pragma unroll
-    for (int q = 0; q < LC; ++q) {
-      if (q < c1) {  // (a guard, not a break: the loop keeps one exit and unrolls fully)
-      const int4 rh = rec[q * 4 + hi];
-      const double a = kcol ? ga[q] : 0.0;
-      double c;
-      if constexpr (MODE != SK_B) {
-        // theta_k(obs lo)[4 hs + hi], the A operand of Z, is the transpose of the gathered tile
-        // theta_k(obs hi)[col]: through the wave's LDS
-        TRl[lane] = gv[q];
-        wave_lds_sync();
-        double z = 0.0;
-#pragma unroll
-        for (int hs = 0; hs < NG; ++hs) {
-          const int h = 4 * hs + hi;
-          const double x = TRl[16 * lo + h];
-          z = mfma4(h < K ? x : 0.0, vb[hs], z);
-        }
-        // Z[obs hi][b = col] = sum_h theta_k(obs hi)[h] V[b][h]; d = eps + sum_b theta_j[b] Z[b]
-        const double dd = row16_sum(a * z) + eps;
-        if constexpr (MODE == SK_LL) {
-          if (col == 0) ll += (double)rh.w * log(dd);
-        } else {
-          c = sk_div((double)rh.w, dd);
-          if (col == 0) {
-            const int2 rr = reinterpret_cast<const int2*>(AUX)[q * 4 + hi];
-            if (rr.x >= 0) {
-              cBb[rr.x] = c;
-              cBb[rr.y] = c;
-            }
-          }
-        }
-      } else {
-        c = AUX[q * 4 + hi];
-      }
-      if constexpr (MODE != SK_LL) {
-        // M += c theta_u (x) theta_v over the chunk's 4 observations (k = observation)
-        m16 = mfma16(a, kcol ? c * gv[q] : 0.0, m16);
-        if (q + 1 == send) {  // stretch t done: its M row into slot t
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int x = hi + 4 * i;
-            if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
-          }
-          m16 = d4v{0.0, 0.0, 0.0, 0.0};
-          ++t;
-          send = stretch_end(t);
-          if constexpr (MODE == SK_A)
+          for (int hs = 0; hs < NG; ++hs) z = mfma4(TRl[16 * lo + 4 * hs + hi], vb[hs], z);
+          const double dd = row16_sum(ga[q] * km * z) + eps;
+          if (col == 0) DL[q * 4 + hi] = dd;
+          if (q + 1 == send) {
+            ++t;
+            send = stretch_end(t);
             if (t < nst) load_v(t);
-        }
-      } else {
-        if (q + 1 == send) {
-          ++t;
-          send = stretch_end(t);
-          if (t < nst) load_v(t);
+          }
         }
       }
+      wave_lds_sync();
+      // ---- one observation per lane: c = n / d (or n log d), once per observation instead of
+      // once per 16 lanes of it
+      const double dl = DL[lane];
+      const double wn = (double)rec[lane].w;
+      const bool real = lane < 4 * c1;
+      if constexpr (MODE == SK_LL) {
+        if (real) ll = wn * log(dl);
+      } else {
+        const double cl = sk_div(wn, dl);
+        DL[lane] = cl;
+        if (MODE == SK_A && real) {
+          const int2 rr = reinterpret_cast<const int2*>(AUX)[lane];
+          if (rr.x >= 0) {
+            cBb[rr.x] = cl;
+            cBb[rr.y] = cl;
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+    if constexpr (MODE != SK_LL) {
+      // ---- M^s += c theta_u (x) theta_v over each chunk's 4 observations (k = observation), c
+      // broadcast from the observation's word; a stretch's M row replaces its V table in slot t
+      const double* __restrict__ cw = MODE == SK_B ? AUX : DL;
+      d4v m16 = d4v{0.0, 0.0, 0.0, 0.0};
+      int t = 0;
+      int send = stretch_end(0);
+#pragma unroll
+      for (int q = 0; q < LC; ++q) {
+        if (q < c1) {
+          m16 = mfma16(ga[q], cw[q * 4 + hi] * gv[q], m16);
+          if (q + 1 == send) {  // stretch t done: its M row into slot t
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int x = hi + 4 * i;
+              if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
+            }
+            m16 = d4v{0.0, 0.0, 0.0, 0.0};
+            ++t;
+            send = stretch_end(t);
+          }
+        }
       }
     }
     st_.mark(2);
+  }
+  if constexpr (MODE != SK_LL) __syncthreads();  // every wave's share of P^s staged
+  if (un.nst > 0) {
+    const int nst = un.nst;
+    const auto& ts = un.ts;
     if constexpr (MODE != SK_LL) {
-      wave_lds_sync();
       // ---- X_q[z] = sum_cell P^s[z][cell] M_q[cell] for the unit's rows q (m = q, n = z in the
       // block's z tile, k = 4 cells per step)
       // (four independent accumulator chains over the cell steps, added in a fixed order)
       double xa[4] = {0.0, 0.0, 0.0, 0.0};
       const int z = 4 * blk + lo;
+      const double* __restrict__ pz = PV + (z < K ? z : K - 1) * K2 + hi;  // B: P^s[z][4 ks + hi]
 #pragma unroll
       for (int ks = 0; ks < NCT; ++ks) {
-        const int cell = 4 * ks + hi;
-        const bool ok = lo < nst && cell < K2;
-        const double am = MSl[ok ? lo * SLOT + cell : 0];
-        xa[ks & 3] = mfma4(ok ? am : 0.0, Ps[ks * 64 + lane], xa[ks & 3]);
+        // (M words past K^2 are zero; rows q >= nst and columns z >= K are not stored)
+        xa[ks & 3] = mfma4(MSl[lo * SLOT + 4 * ks + hi], pz[4 * ks], xa[ks & 3]);
       }
       const double xacc = (xa[0] + xa[1]) + (xa[2] + xa[3]);
       if (hi < nst && blk < NG && z < K) xb[(size_t)un.prow * K + z] = xacc;
-      if constexpr (MODE == SK_A) {
+      if (MODE == SK_A || (MODE == SK_U && s == 0)) {
         // ---- S_r[a][cell] += sum_q theta_{g_q}[a] M_q[cell] (m = a, k = q, n = cell)
 #pragma unroll
         for (int cg = 0; cg < NCG; ++cg) {
-          const int cell = 4 * (4 * cg + blk) + lo;
-          const bool ok = hi < nst && cell < K2;
-          const double mb = MSl[ok ? hi * SLOT + cell : 0];
+          // (ts is zero for q = hi >= nst; cells >= K^2 are not stored)
+          const double mb = MSl[hi * SLOT + 4 * (4 * cg + blk) + lo];
 #pragma unroll
-          for (int at = 0; at < NG; ++at) sacc[at][cg] = mfma4(ts[at], ok ? mb : 0.0, 0.0);
+          for (int at = 0; at < NG; ++at) sacc[at][cg] = mfma4(ts[at], mb, 0.0);
         }
       }
       st_.mark(3);
     }
   }
 
-  if constexpr (MODE == SK_A) {
+  if (MODE == SK_A || (MODE == SK_U && s == 0)) {  // (workgroup-uniform)
     // ---- the workgroup's S partial: the 8 waves' shares added in a fixed order,
-    // ((w0 + w4) + (w2 + w6)) + ((w1 + w5) + (w3 + w7)), through LDS
+    // ((w0 + w4) + (w2 + w6)) + ((w1 + w5) + (w3 + w7)), through LDS: waves 4-7 park theirs, waves
+    // 0-3 add them to their own and park the pair sums, then every thread combines the four pairs
+    // for its share of the K^3 partial and stores it
+    constexpr int NE = NG * NCG * 64;  // (a tile, cell group, lane) entries of one share
     double* red = smem;
     auto put = [&](int slot) {
 #pragma unroll
       for (int at = 0; at < NG; ++at)
 #pragma unroll
-        for (int cg = 0; cg < NCG; ++cg) red[((slot * NG + at) * NCG + cg) * 64 + lane] = sacc[at][cg];
-    };
-    auto add = [&](int slot) {
-#pragma unroll
-      for (int at = 0; at < NG; ++at)
-#pragma unroll
-        for (int cg = 0; cg < NCG; ++cg) sacc[at][cg] += red[((slot * NG + at) * NCG + cg) * 64 + lane];
+        for (int cg = 0; cg < NCG; ++cg) red[slot * NE + (at * NCG + cg) * 64 + lane] = sacc[at][cg];
     };
     __syncthreads();
     if (wv >= 4) put(wv - 4);
     __syncthreads();
-    if (wv < 4) add(wv);
-    __syncthreads();
-    if (wv == 2 || wv == 3) put(wv - 2);
-    __syncthreads();
-    if (wv < 2) add(wv);
-    __syncthreads();
-    if (wv == 1) put(0);
-    __syncthreads();
-    if (wv == 0) {
-      add(0);
-      double* __restrict__ out = spart + ((size_t)b * n_wg + w) * K3;
+    if (wv < 4) {
 #pragma unroll
       for (int at = 0; at < NG; ++at)
 #pragma unroll
-        for (int cg = 0; cg < NCG; ++cg) {
-          const int a = 4 * at + hi, cell = 4 * (4 * cg + blk) + lo;
-          if (a < K && cell < K2) out[a * K2 + cell] = sacc[at][cg];
-        }
+        for (int cg = 0; cg < NCG; ++cg) sacc[at][cg] += red[wv * NE + (at * NCG + cg) * 64 + lane];
+      put(wv);
+    }
+    __syncthreads();
+    double* __restrict__ out = spart + ((size_t)b * n_wg + w) * K3;
+#pragma unroll
+    for (int i = 0; i < (NE + NT - 1) / NT; ++i) {
+      const int e = tid + NT * i;
+      if (e < NE) {
+        const int l = e & 63, ac = e >> 6;
+        const int a = 4 * (ac / NCG) + (l >> 4), cell = 4 * (4 * (ac % NCG) + ((l >> 2) & 3)) + (l & 3);
+        const double v = (red[e] + red[2 * NE + e]) + (red[NE + e] + red[3 * NE + e]);
+        if (a < K && cell < K2) out[a * K2 + cell] = v;
+      }
     }
   }
   if constexpr (MODE == SK_LL) {
@@ -409,7 +432,7 @@ __global__ __launch_bounds__(NT) void sk_pass_kernel(
     }
   }
   st_.mark(7);
-  st_.flush(MODE == SK_B ? 1 : MODE == SK_A ? 0 : 4, ((long long)b * gridDim.x + w) * NW + wv, lane);
+  st_.flush(MODE == SK_B ? 1 : MODE == SK_LL ? 4 : 0, ((long long)b * gridDim.x + wx) * NW + wv, lane);
 }
 
 // ------------------------------------------------------------------------------------------
