@@ -37,9 +37,9 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
       return fail("wg units", w, pl.wg_ustart[w + 1] - pl.wg_ustart[w]);
     for (int u = pl.wg_ustart[w]; u < pl.wg_ustart[w + 1]; ++u) {
       const int* d = &pl.udesc[(size_t)u * UD];
-      if (d[14] != pl.wg_code[w]) return fail("unit code", u, d[14]);
-      const int nst = d[5], c0 = d[0], c1 = d[4];
-      if (nst < 1 || nst > GU) return fail("stretches", u, nst);
+      if (d[D_CODE] != pl.wg_code[w]) return fail("unit code", u, d[D_CODE]);
+      const int nst = d[D_NST], c0 = d[0], c1 = d[D_END];
+      if (nst < 1 || nst > pl.gu) return fail("stretches", u, nst);
       if (c1 - c0 > LCAP_SK || c1 <= c0) return fail("unit length", u, c1 - c0);
       for (int t = 0; t < GU; ++t) {
         const int a = d[t], b = t + 1 < nst ? d[t + 1] : c1;
@@ -48,9 +48,9 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
           continue;
         }
         if (b <= a) return fail("stretch order", u, t);
-        const int q = d[6 + t], g = d[10 + t];
+        const int q = d[D_PROW + t], g = d[D_GENE + t];
         if (q < 0 || q >= pl.n_prows || pl.prow_gene[q] != g) return fail("stretch prow", u, t);
-        if (t > 0 && d[10 + t - 1] == g) return fail("stretch not maximal", u, t);
+        if (t > 0 && d[D_GENE + t - 1] == g) return fail("stretch not maximal", u, t);
         for (int c = a; c < b; ++c) {
           covered[c]++;
           if (pl.chunk_prow[c] != q) return fail("chunk prow", c, q);
@@ -95,13 +95,13 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
     for (long long slot = 0; slot < pl.sk_slots[g]; ++slot) {
       const int* d = &pl.sk_udesc[g][(size_t)slot * UD];
       const int w = w0 + (int)(slot / per);
-      if (d[14] != pl.wg_code[w]) return fail("slot code", slot, d[14]);
-      if (d[5] == 0) continue;
+      if (d[D_CODE] != pl.wg_code[w]) return fail("slot code", slot, d[D_CODE]);
+      if (d[D_NST] == 0) continue;
       ++units_seen;
       const int u = pl.wg_ustart[w] + (int)(slot % per);
       const int* du = &pl.udesc[(size_t)u * UD];
-      if (d[4] != du[4] - du[0] || d[4] > L || d[0] != 0) return fail("slot extent", slot, d[4]);
-      for (int i = 0; i < 4 * d[4]; ++i) {
+      if (d[D_END] != du[D_END] - du[0] || d[D_END] > L || d[0] != 0) return fail("slot extent", slot, d[D_END]);
+      for (int i = 0; i < 4 * d[D_END]; ++i) {
         const I4& a = pl.sk_urec[g][(size_t)slot * 4 * L + i];
         const I4& b = pl.rows[4LL * du[0] + i];
         // group 1 (streams 1, 2) carries the observation's count n = its stream-0 row's w (0: padding)
@@ -146,16 +146,18 @@ int main() {
     for (int r = 0; r < R; ++r)
       if (scanf("%d", &counts[e * R + r]) != 1) return fail("counts");
   }
-  // gcap 0: the small-K plan of sk.h (sp_rows = its wg_target); -1: the same, fill-packed (fused launch)
-  const bool small = gcap <= 0, fill = gcap < 0;
-  const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill)
+  // gcap <= 0: the small-K plans of sk.h (sp_rows = their wg_target): 0 = 4 stretches per unit
+  // (K 11-12), -3 = 8 (K <= 10); fill-packed (the fused launch) -1 = 8, -2 = 4
+  const bool small = gcap <= 0, fill = gcap == -1 || gcap == -2;
+  const int gu = (gcap == 0 || gcap == -2) ? 4 : 8;
+  const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill, gu)
                         : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows);
   if (fill) {  // every unit but the last of its (stream, rating) section is full: LCAP_SK chunks or GU stretches
     for (long long u = 0; u + 1 < pl.n_units; ++u) {
       const int* d = &pl.udesc[(size_t)u * UD];
       const int* dn = &pl.udesc[(size_t)(u + 1) * UD];
-      if (dn[14] != d[14]) continue;  // the section's last unit
-      if (d[4] - d[0] != LCAP_SK && d[5] != GU) return fail("fill", (int)u, d[4] - d[0]);
+      if (dn[D_CODE] != d[D_CODE]) continue;  // the section's last unit
+      if (d[D_END] - d[0] != LCAP_SK && d[D_NST] != pl.gu) return fail("fill", (int)u, d[D_END] - d[0]);
     }
   }
 

@@ -55,10 +55,13 @@ def _links(P, E, seed, R=2, hub=0.0, multi=0.05, both=0.03):
     (40, 600, (1, 1), 0, 1024, 0.0),           # one unit per stream: runs split at 32 chunks
     (200, 6000, (64, 64), 0, 3, 5.0),          # long units (16 chunks)
     (30, 1500, (1536, 3072), 0, 1024, 0.0),    # more units than chunks
-    # fill-packed small-K plans (gcap -1: the fused launch): full units, runs split at unit ends
+    (200, 6000, (64, 64), -3, 3, 5.0),         # 8 stretches per unit (K <= 10)
+    # fill-packed small-K plans (gcap -1 / -2: the fused launch, 8 / 4 stretches): full units, runs
+    # split at unit ends
     (300, 5000, (1, 1), -1, 1024, 30.0),       # hub genes
     (1500, 20000, (1, 1), -1, 1024, 0.0),      # fold0-like degree
     (40, 600, (1, 1), -1, 1024, 0.0),          # few genes: long runs
+    (1500, 20000, (1, 1), -2, 1024, 0.0),      # 4 stretches (K = 11, 12)
 ])
 def test_plan_invariants(plan_check, P, E, units, gcap, sp_rows, hub):
     links = _links(P, E, seed=P + E, hub=hub)

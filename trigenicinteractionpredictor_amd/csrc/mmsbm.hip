@@ -1684,7 +1684,8 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
     }
   }
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
-                           c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, 1024, c->sk_fused);
+                           c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, 1024, c->sk_fused,
+                           mmsbm_plan::sk_gu(c->K));
   const auto& h = sd.h;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;
@@ -1999,7 +2000,7 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[5] = h.n_sp;
   info[6] = h.n_prows;
   info[9] = h.prow_ptr.empty() ? 0 : h.prow_ptr[(size_t)h.R * (h.P + 1)];  // stream-0 partial rows
-  info[7] = h.small ? mmsbm_plan::GU : h.gmax;
+  info[7] = h.small ? h.gu : h.gmax;
   info[8] = h.small ? info[9] : (int64_t)h.vgenes.size();  // small-K: one V table per stream-0 stretch
   info[10] = h.small ? 1 : 0;
   info[11] = h.small ? h.n_units : (int64_t)(h.n_wg_a + h.n_wg_b) * NW;

@@ -26,12 +26,20 @@ namespace mmsbm_plan {
 
 constexpr int CH = 4;   // observations per chunk (one MFMA k-step)
 constexpr int NW = 8;   // waves (units) per workgroup
-// Small-K plans (K <= 12, the register-direct kernels of sk.h): a unit has at most GU gene
-// stretches (one wave keeps their V tables and M rows, and contracts them with p at its end) and
-// at most LCAP_SK chunks (its records are staged in the wave's LDS at once).
-constexpr int GU = 4;
+// Small-K plans (K <= 12, the register-direct kernels of sk.h): a unit has at most `gu` <= GU gene
+// stretches (one wave keeps their V tables and M rows, and contracts them with p at its end; gu is
+// the kernel's LDS budget: 8 at K <= 10, 4 above) and at most LCAP_SK chunks (its records are staged
+// in the wave's LDS at once).
+constexpr int GU = 8;
 constexpr int LCAP_SK = 16;
-constexpr int UD = 16;  // ints per unit descriptor (below)
+// unit descriptor: stretch start chunks [0, GU) (unused ones = the end), end chunk [D_END], stretches
+// [D_NST], partial rows [D_PROW, +GU), pivot genes [D_GENE, +GU), stream * 16 + rating [D_CODE]
+constexpr int D_END = GU, D_NST = GU + 1, D_PROW = GU + 2, D_GENE = 2 * GU + 2, D_CODE = 3 * GU + 2;
+constexpr int UD = 32;  // ints per unit descriptor
+static_assert(D_CODE < UD, "descriptor layout");
+// stretches per unit of the small-K kernels at K (their LDS budget: GU * K^2 words of V tables / M
+// rows per wave fit two workgroups per CU up to K = 10)
+constexpr int sk_gu(int K) { return K <= 10 ? 8 : 4; }
 
 struct I4 {
   int x, y, z, w;
@@ -53,9 +61,8 @@ struct Plan {
   int sp_lo[8] = {0}, sp_hi[8] = {0};  // S-partial workgroups of each rating
   // small-K plans only (sk.h):
   bool small = false;
-  std::vector<int> udesc;          // [n_units][UD]: stretch start chunks [0..3], end chunk [4],
-                                   // stretches [5], partial rows [6..9], pivot genes [10..13],
-                                   // stream * 16 + rating [14]
+  int gu = GU;                     // most stretches per unit (<= GU)
+  std::vector<int> udesc;          // [n_units][UD]: the unit descriptors (D_* offsets above)
   std::vector<int> wg_ustart;      // [n_wg + 1] units of each workgroup (rounds of NW)
   std::vector<int> row12;          // [n_rows0][2] the observation's stream-1 / stream-2 row
                                    // (relative to n_rows0; -1 on padding rows)
@@ -67,9 +74,8 @@ struct Plan {
   // capacity of 4 L rows per slot, so a wave finds its unit's records from its slot number alone.
   int sk_L[2] = {0, 0};            // chunks per slot (the group's longest unit)
   long long sk_slots[2] = {0, 0};
-  std::vector<int> sk_udesc[2];    // [slots][UD]: stretch starts [0..3] and end [4] relative to the
-                                   // slot's first chunk, stretches [5] (0: empty slot), partial rows
-                                   // [6..9], pivot genes [10..13], stream * 16 + rating [14]
+  std::vector<int> sk_udesc[2];    // [slots][UD]: unit descriptors with the stretch starts and end
+                                   // relative to the slot's first chunk (D_NST 0: empty slot)
   std::vector<I4> sk_urec[2];      // [slots][4 L] records
   std::vector<int> sk_urow12;      // [slots_0][4 L][2] slot-major row of the stream-1 / stream-2 copy
                                    // of each stream-0 row (-1: padding), the index of its c in pass B
@@ -137,7 +143,7 @@ inline void make_slots(Plan& pl) {
     for (int w = w0; w < w1; ++w)
       for (int u = pl.wg_ustart[w]; u < pl.wg_ustart[w + 1]; ++u) {
         const int* d = &pl.udesc[(size_t)u * UD];
-        L = std::max(L, d[4] - d[0]);
+        L = std::max(L, d[D_END] - d[0]);
       }
     pl.sk_L[g] = L;
     pl.sk_slots[g] = (long long)(w1 - w0) * per;
@@ -149,15 +155,15 @@ inline void make_slots(Plan& pl) {
         int* sd = &pl.sk_udesc[g][(size_t)slot * UD];
         const int u = pl.wg_ustart[w] + k;
         if (u >= pl.wg_ustart[w + 1]) {  // empty slot
-          sd[14] = pl.wg_code[w];
+          sd[D_CODE] = pl.wg_code[w];
           continue;
         }
         const int* d = &pl.udesc[(size_t)u * UD];
         const int c0 = d[0];
         for (int t = 0; t < UD; ++t) sd[t] = d[t];
-        for (int t = 0; t < 5; ++t) sd[t] = d[t] - c0;
+        for (int t = 0; t <= D_END; ++t) sd[t] = d[t] - c0;
         I4* rec = &pl.sk_urec[g][(size_t)slot * 4 * L];
-        const long long row0 = 4LL * c0, nrow = 4LL * (d[4] - c0);
+        const long long row0 = 4LL * c0, nrow = 4LL * (d[D_END] - c0);
         for (long long i = 0; i < 4LL * L; ++i) {
           const long long row = row0 + (i < nrow ? i : nrow - 1);  // padding: the unit's last row
           rec[i] = pl.rows[row];
@@ -187,8 +193,9 @@ inline void make_slots(Plan& pl) {
 // K^3 partial, so large K wants more rows per partial).
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
-                  int wg_target = 1024, bool fill = false) {
+                  int wg_target = 1024, bool fill = false, int gu = GU) {
   Plan pl;
+  pl.gu = std::max(1, std::min(gu, GU));
   pl.R = R;
   pl.P = P;
   pl.streams = em ? 3 : 1;
@@ -276,7 +283,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       }
       // units
       std::vector<int> ub;
-      pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? GU : s == 0 ? gcap : (1 << 30), ub,
+      pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? pl.gu : s == 0 ? gcap : (1 << 30), ub,
                  small && fill);
       const int nunits = (int)ub.size() - 1;
       // chunk -> gene
@@ -298,18 +305,18 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
           for (int c = c0; c < c1; ++c)
             if (c == c0 || cgene[c] != cgene[c - 1]) {
               d[nst] = chunk_base + c;      // stretch start
-              d[10 + nst] = cgene[c];       // its pivot gene
+              d[D_GENE + nst] = cgene[c];   // its pivot gene
               ++nst;
             }
           for (int t = nst; t < GU; ++t) {
             d[t] = chunk_base + c1;
-            d[10 + t] = cgene[c0];
+            d[D_GENE + t] = cgene[c0];
           }
-          d[4] = chunk_base + c1;
-          d[5] = nst;
-          for (int t = 0; t < GU; ++t) d[6 + t] = -1;  // partial rows: filled below (em plans)
-          d[14] = s * 16 + r;
-          d[15] = 0;
+          d[D_END] = chunk_base + c1;
+          d[D_NST] = nst;
+          for (int t = 0; t < GU; ++t) d[D_PROW + t] = -1;  // partial rows: filled below (em plans)
+          d[D_CODE] = s * 16 + r;
+          for (int t = D_CODE + 1; t < UD; ++t) d[t] = 0;
           pl.udesc.insert(pl.udesc.end(), d, d + UD);
         }
         pl.n_units += nunits;
@@ -382,7 +389,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
           const long long u_first = pl.n_units - (long long)(ub.size() - 1);
           for (int u = 0; u + 1 < (int)ub.size(); ++u) {
             int* d = &pl.udesc[(size_t)(u_first + u) * UD];
-            for (int t = 0; t < d[5]; ++t) d[6 + t] = pl.chunk_prow[(size_t)d[t]];
+            for (int t = 0; t < d[D_NST]; ++t) d[D_PROW + t] = pl.chunk_prow[(size_t)d[t]];
           }
         }
         // CSR over genes: prows of stream (s, r) ascend by gene

@@ -4,7 +4,7 @@
 // sk_pass_kernel<K, SK_LL> + reduce_kernel.  Same pivot-run algebra as the large-K kernels
 // (mmsbm.hip header), laid out for latency instead of throughput:
 //
-//  * one unit (<= GU gene stretches, <= LCAP_SK chunks of 4 observations) per wave, and no
+//  * one unit (<= GUK gene stretches, <= LCAP_SK chunks of 4 observations) per wave, and no
 //    workgroup barrier between a wave's start and its end: the wave stages its unit's records in
 //    its own LDS with one coalesced load, computes the V tables of its own <= 4 pivot genes
 //    (one MFMA per (a tile, cell group), p_r staged once per workgroup), and gathers the theta
@@ -48,7 +48,9 @@ struct SKT {
   // unguarded V-operand reads touch (rows a >= K of the 4-wide a tiles, cells up to 16 NCG)
   static constexpr int PVR = (4 * NG - 1) * K2 + 16 * NCG;
   static constexpr int PSD = ((PVR > K3 ? PVR : K3) + 1) & ~1;
-  static constexpr int WAVE = mmsbm_plan::GU * SLOT + 2 * SK_ROWS + SK_ROWS + 64 + SK_ROWS;  // slots,
+  static constexpr int GUK = mmsbm_plan::sk_gu(K);  // stretches per unit (slots per wave): 8 or 4
+  static constexpr int NT2 = GUK / 4;                // 4-row MFMA tiles of the unit's stretches
+  static constexpr int WAVE = GUK * SLOT + 2 * SK_ROWS + SK_ROWS + 64 + SK_ROWS;  // slots,
                                                              // records, aux, transpose, d / c words
   static constexpr int WAVE_B = WAVE - 64 - SK_ROWS;  // pass B: c arrives in aux
   static constexpr int LDS_B = (PSD + NW * WAVE_B) * 8;
@@ -59,10 +61,13 @@ struct SKT {
   static constexpr int LDS = (PSD + NW * WAVE) * 8;
   static_assert(K <= 12, "small-K kernels: K <= 12");
   static_assert(4 * NS * 64 <= PSD + NW * WAVE_U, "S reduction buffer over the LDS");
-  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+  static_assert(LDS_U <= 80 * 1024, "two fused / likelihood workgroups per CU");
+  static_assert(LDS <= 160 * 1024, "pass A LDS");
+  static_assert(GUK % 4 == 0 && GUK <= mmsbm_plan::GU, "stretch tiles");
+  static_assert(GUK * 4 * NG <= 2 * SK_ROWS, "pivot-gene theta rows over the records");
   static_assert(SLOT >= 4 * NCT, "slot holds a V table / M row");
   // the unguarded V / M reads stay inside the slots and the records (finite words)
-  static_assert((mmsbm_plan::GU - 1) * SLOT + 15 * K + 4 * NG <= mmsbm_plan::GU * SLOT + 2 * SK_ROWS,
+  static_assert((GUK - 1) * SLOT + 15 * K + 4 * NG <= GUK * SLOT + 2 * SK_ROWS,
                 "V reads past the wave's slots and records");
   static_assert(16 * NCG <= SLOT + 2 * SK_ROWS, "S operand reads past the slots and records");
 };
@@ -123,9 +128,10 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
   double* PV = smem;  // P^s_r[z][cell] (cell = x K + y over the u, v slots), zero past K^3
   double* wl = smem + T::PSD + wv * (MODE == SK_B ? T::WAVE_B : MODE == SK_U ? T::WAVE_U : T::WAVE);
-  double* MSl = wl;                                                 // GU slots: V, then M
-  int4* REC = reinterpret_cast<int4*>(wl + mmsbm_plan::GU * SLOT);  // the unit's records
-  double* AUX = wl + mmsbm_plan::GU * SLOT + 2 * SK_ROWS;           // row12 (A) / c (B)
+  constexpr int GUK = T::GUK, NT2 = T::NT2;
+  double* MSl = wl;                                                 // GUK slots: V, then M
+  int4* REC = reinterpret_cast<int4*>(wl + GUK * SLOT);             // the unit's records
+  double* AUX = wl + GUK * SLOT + 2 * SK_ROWS;                      // row12 (A) / c (B)
   double* TRl = MODE == SK_U ? AUX : AUX + SK_ROWS;                 // Z operand transpose
   double* DL = TRl + 64;                                            // d, then c, per observation
   double* __restrict__ cBb = cB + (size_t)b * n_cb;
@@ -150,21 +156,21 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
 
   // One slot's descriptor, records (+ row12 / c) and pivot-gene theta, loaded together.
   struct Unit {
-    int nst, d1, d2, d3, c1, prow;
+    int nst, c1, ds[GUK], prow[NT2];
     int4 rv[RPL];
     int2 r12[RPL];
     double cv[RPL];
-    double tv[NG], ts[NG];  // theta_{gene lo}[4 as + hi] (V), theta_{gene hi}[4 at + lo] (S)
+    double tv[NT2][NG];     // theta_{gene 4 tt + lo}[4 as + hi] (A of V; zero past nst and K)
   };
   auto load_unit = [&](Unit& un) {
     const long long slot = (long long)w * NW + wv;
     const int* __restrict__ d = udesc + slot * mmsbm_plan::UD;
-    un.nst = __builtin_amdgcn_readfirstlane(d[5]);  // wave-uniform (scalar control flow)
-    un.d1 = __builtin_amdgcn_readfirstlane(d[1]);
-    un.d2 = __builtin_amdgcn_readfirstlane(d[2]);
-    un.d3 = __builtin_amdgcn_readfirstlane(d[3]);
-    un.c1 = __builtin_amdgcn_readfirstlane(d[4]);
-    un.prow = d[6 + hi];
+    un.nst = __builtin_amdgcn_readfirstlane(d[mmsbm_plan::D_NST]);  // wave-uniform (scalar control flow)
+    un.c1 = __builtin_amdgcn_readfirstlane(d[mmsbm_plan::D_END]);
+#pragma unroll
+    for (int t = 0; t < GUK; ++t) un.ds[t] = __builtin_amdgcn_readfirstlane(d[t]);
+#pragma unroll
+    for (int tt = 0; tt < NT2; ++tt) un.prow[tt] = d[mmsbm_plan::D_PROW + 4 * tt + hi];
     const int nrow = 4 * L;  // the slot's capacity (every row valid: make_slots pads), so the record
                              // loads do not wait for the descriptor
     const long long rbase = slot * 4 * L;
@@ -177,14 +183,15 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
       if constexpr (MODE == SK_B) un.cv[i] = cBb[row];
     }
     if constexpr (MODE != SK_B) {
-      const int glo = d[10 + lo], ghi = d[10 + hi];
 #pragma unroll
-      for (int as = 0; as < NG; ++as) {
-        const int a1 = 4 * as + hi, a2 = 4 * as + lo;
-        const double v1 = th[(size_t)glo * K + (a1 < K ? a1 : 0)];
-        const double v2 = th[(size_t)ghi * K + (a2 < K ? a2 : 0)];
-        un.tv[as] = (lo < un.nst && a1 < K) ? v1 : 0.0;
-        un.ts[as] = (hi < un.nst && a2 < K) ? v2 : 0.0;
+      for (int tt = 0; tt < NT2; ++tt) {
+        const int glo = d[mmsbm_plan::D_GENE + 4 * tt + lo];
+#pragma unroll
+        for (int as = 0; as < NG; ++as) {
+          const int a1 = 4 * as + hi;
+          const double v1 = th[(size_t)glo * K + (a1 < K ? a1 : 0)];
+          un.tv[tt][as] = (4 * tt + lo < un.nst && a1 < K) ? v1 : 0.0;
+        }
       }
     }
   };
@@ -220,12 +227,15 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
 
   if (un.nst > 0) {  // an empty slot only joins the workgroup's barriers
     const int nst = un.nst;
-    const int c0 = 0, d1 = un.d1, d2 = un.d2, d3 = un.d3, c1 = un.c1;
+    const int c0 = 0, c1 = un.c1;
     st_.t[5] = (unsigned long long)(c1 - c0);
     st_.t[4] = (unsigned long long)nst;
-    auto stretch_end = [=](int t) {  // first chunk after stretch t (values: no pointer select)
+    const auto& ds = un.ds;
+    auto stretch_end = [&](int t) {  // first chunk after stretch t (scalar selects, constant indices)
       int e = c1;
-      if (t + 1 < nst) e = t == 0 ? d1 + 0 : t == 1 ? d2 + 0 : d3 + 0;
+#pragma unroll
+      for (int i = 1; i < GUK; ++i)
+        if (t + 1 == i && i < nst) e = ds[i];
       return e;
     };
     // ---- theta gathers.  Every theta value the unit needs is gathered at once, straight into the
@@ -251,6 +261,10 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
     };
 #pragma unroll
     for (int i = 0; i < LC; ++i) gather(i);
+    const int wlane = rec[lane].w;  // this lane's observation's count (the records die here)
+    // the unit's pivot-gene theta rows, [GUK][4 NG] words over the records (read in order after
+    // them: a wave's LDS operations complete in order), the S contraction's A operand
+    double* THl = reinterpret_cast<double*>(REC);
     const auto& tv = un.tv;  // (array references: the indices stay compile-time constants)
     if constexpr (MODE != SK_B) {
       // ---- V_g[cell] = sum_a theta_g[a] P^s[a][cell] for the unit's genes (m = gene, k = a, B
@@ -258,18 +272,30 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
       // of the wave's LDS (cell = b K + h).  Every word of the GU slots is written (zero past K^2
       // and for absent stretches), so the unguarded V / M reads below see finite values.
 #pragma unroll
-      for (int cg = 0; cg < NCG; ++cg) {
-        const int cell = 4 * (4 * cg + blk) + lo;
-        double v = 0.0;
+      for (int tt = 0; tt < NT2; ++tt) {
+        const bool live = tt == 0 || nst > 4 * tt;  // (uniform) a tile without stretches: zeros
 #pragma unroll
-        for (int as = 0; as < NG; ++as) v = mfma4(tv[as], PV[(4 * as + hi) * K2 + cell], v);
-        if (cell < SLOT) MSl[hi * SLOT + cell] = cell < K2 ? v : 0.0;
+        for (int cg = 0; cg < NCG; ++cg) {
+          const int cell = 4 * (4 * cg + blk) + lo;
+          double v = 0.0;
+          if (live) {
+#pragma unroll
+            for (int as = 0; as < NG; ++as) v = mfma4(tv[tt][as], PV[(4 * as + hi) * K2 + cell], v);
+          }
+          if (cell < SLOT) MSl[(4 * tt + hi) * SLOT + cell] = cell < K2 ? v : 0.0;
+        }
+#pragma unroll
+        for (int as = 0; as < NG; ++as)
+          if (blk == 0) THl[(4 * tt + lo) * 4 * NG + 4 * as + hi] = tv[tt][as];
+        // (one tile's operand reads in flight at a time: beside the LC chunks' gathers, both tiles'
+        // would not fit the register budget)
+        __builtin_amdgcn_sched_barrier(0);
       }
     } else {
       // pass B forms no V tables: the slots' words past each M row stay finite (zero)
 #pragma unroll
-      for (int i = 0; i < (mmsbm_plan::GU * SLOT + 63) / 64; ++i)
-        if (lane + 64 * i < mmsbm_plan::GU * SLOT) MSl[lane + 64 * i] = 0.0;
+      for (int i = 0; i < (GUK * SLOT + 63) / 64; ++i)
+        if (lane + 64 * i < GUK * SLOT) MSl[lane + 64 * i] = 0.0;
     }
     wave_lds_sync();
     st_.mark(1);
@@ -308,7 +334,7 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
       // ---- one observation per lane: c = n / d (or n log d), once per observation instead of
       // once per 16 lanes of it
       const double dl = DL[lane];
-      const double wn = (double)rec[lane].w;
+      const double wn = (double)wlane;
       const bool real = lane < 4 * c1;
       if constexpr (MODE == SK_LL) {
         if (real) ll = wn * log(dl);
@@ -354,29 +380,41 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
   if constexpr (MODE != SK_LL) __syncthreads();  // every wave's share of P^s staged
   if (un.nst > 0) {
     const int nst = un.nst;
-    const auto& ts = un.ts;
+    const double* THl = reinterpret_cast<const double*>(REC);  // (see the unit prologue)
     if constexpr (MODE != SK_LL) {
       // ---- X_q[z] = sum_cell P^s[z][cell] M_q[cell] for the unit's rows q (m = q, n = z in the
       // block's z tile, k = 4 cells per step)
       // (four independent accumulator chains over the cell steps, added in a fixed order)
-      double xa[4] = {0.0, 0.0, 0.0, 0.0};
       const int z = 4 * blk + lo;
       const double* __restrict__ pz = PV + (z < K ? z : K - 1) * K2 + hi;  // B: P^s[z][4 ks + hi]
 #pragma unroll
-      for (int ks = 0; ks < NCT; ++ks) {
-        // (M words past K^2 are zero; rows q >= nst and columns z >= K are not stored)
-        xa[ks & 3] = mfma4(MSl[lo * SLOT + 4 * ks + hi], pz[4 * ks], xa[ks & 3]);
+      for (int tt = 0; tt < NT2; ++tt) {
+        if (tt == 0 || nst > 4 * tt) {  // (uniform)
+          double xa[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int ks = 0; ks < NCT; ++ks) {
+            // (M words past K^2 are zero; rows q >= nst and columns z >= K are not stored)
+            xa[ks & 3] = mfma4(MSl[(4 * tt + lo) * SLOT + 4 * ks + hi], pz[4 * ks], xa[ks & 3]);
+          }
+          const double xacc = (xa[0] + xa[1]) + (xa[2] + xa[3]);
+          if (4 * tt + hi < nst && blk < NG && z < K) xb[(size_t)un.prow[tt] * K + z] = xacc;
+        }
       }
-      const double xacc = (xa[0] + xa[1]) + (xa[2] + xa[3]);
-      if (hi < nst && blk < NG && z < K) xb[(size_t)un.prow * K + z] = xacc;
       if (MODE == SK_A || (MODE == SK_U && s == 0)) {
-        // ---- S_r[a][cell] += sum_q theta_{g_q}[a] M_q[cell] (m = a, k = q, n = cell)
+        // ---- S_r[a][cell] += sum_q theta_{g_q}[a] M_q[cell] (m = a, k = q, n = cell), the
+        // unit's row tiles in order
 #pragma unroll
-        for (int cg = 0; cg < NCG; ++cg) {
-          // (ts is zero for q = hi >= nst; cells >= K^2 are not stored)
-          const double mb = MSl[hi * SLOT + 4 * (4 * cg + blk) + lo];
+        for (int tt = 0; tt < NT2; ++tt) {
+          if (tt == 0 || nst > 4 * tt) {
 #pragma unroll
-          for (int at = 0; at < NG; ++at) sacc[at][cg] = mfma4(ts[at], mb, 0.0);
+            for (int cg = 0; cg < NCG; ++cg) {
+              // (ts is zero for q >= nst; cells >= K^2 are not stored)
+              const double mb = MSl[(4 * tt + hi) * SLOT + 4 * (4 * cg + blk) + lo];
+#pragma unroll
+              for (int at = 0; at < NG; ++at)  // A: theta_{g_q}[4 at + lo] for q = 4 tt + hi
+                sacc[at][cg] = mfma4(THl[(4 * tt + hi) * 4 * NG + 4 * at + lo], mb, sacc[at][cg]);
+            }
+          }
         }
       }
       st_.mark(3);
