@@ -108,6 +108,8 @@ def spawn_ranks(n):
 
 
 KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, d, c, M0 on FP64 MFMA)",
+                "fused": "sk_pass_kernel<%d, SK_U> (fused E-step, all 3 streams: V, Z, d, c, M, X; "
+                         "stream-0 S partials; FP64 MFMA)",
                 "pass_b": "pass_kernel<%d, PASS_B> (streams 1/2: M1, M2; S partials)",
                 "fin": "fin_kernel<%d> (per-gene X contractions, theta and p update)"}
 
@@ -123,6 +125,16 @@ def kernel_work(plan, K, P, R, B, E_obs):
     prow0 = plan["partial_rows_stream0"]
     genes_a = plan["v_genes"]
     params = 8.0 * (P * K + R * K3)
+    if plan.get("small_k") == 2:
+        # the fused small-K E-step (csrc/sk.h SK_U): every stream's observations get Z, d, c and
+        # M (each stream forms its own c); per stretch of any stream a V table and an X
+        # contraction, per stream-0 stretch an S update; bytes: all records, X partials, S partials
+        wga = plan["wg_stream0"]
+        u_fl = 3.0 * E_obs * (4.0 * K2 + 2.0 * K) + prows * 2 * 2.0 * K3 + prow0 * 2.0 * K3
+        u_by = 16.0 * rows + 8.0 * K * prows + 8.0 * K3 * wga + params
+        f_fl = 1.0 * prows * K + R * K3 * wga + 3.0 * P * K + 3.0 * R * K3
+        f_by = 8.0 * K * prows + 8.0 * K3 * wga + 2 * params + 4.0 * 6 * P
+        return {"pass_a": (u_fl * B, u_by * B), "pass_b": (0.0, 0.0), "fin": (f_fl * B, f_by * B)}
     if plan.get("small_k"):
         # small-K kernels (csrc/sk.h): per stream-0 stretch a V table, an X contraction and an S
         # update (2K^3 each); per stream-1/2 stretch an X contraction; bytes: records, row12 and
@@ -203,7 +215,8 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
             "hbm": {"bytes_per_iteration": b8, "achieved": b8 / iter_s / 1e9, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": b8 / iter_s / 1e9 / HBM_PEAK_GBS,
                     "traffic_over_compulsory": None if traffic is None else traffic / b8},
-            "dominant_kernel": {"kernel": KERNEL_NAMES[dom] % K, "avg_launch_us": dom_s * 1e6,
+            "dominant_kernel": {"kernel": KERNEL_NAMES["fused" if plan.get("small_k") == 2 and dom == "pass_a"
+                                                    else dom] % K, "avg_launch_us": dom_s * 1e6,
                                 "executed_flops_per_launch": dfl, "algorithmic_bytes_per_launch": dby,
                                 "tflops": dfl / dom_s / 1e12, "mfma_frac": dfl / dom_s / 1e12 / FP64_PEAK_TFLOPS,
                                 "gbs": dby / dom_s / 1e9, "hbm_frac": dby / dom_s / 1e9 / HBM_PEAK_GBS,

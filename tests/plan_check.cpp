@@ -104,9 +104,12 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
       for (int i = 0; i < 4 * d[D_END]; ++i) {
         const I4& a = pl.sk_urec[g][(size_t)slot * 4 * L + i];
         const I4& b = pl.rows[4LL * du[0] + i];
-        // group 1 (streams 1, 2) carries the observation's count n = its stream-0 row's w (0: padding)
+        // (u, v, pivot, n) in the stream's order; group 1 (streams 1, 2) carries the observation's
+        // count n = its stream-0 row's w (0: padding)
         const int bw = g == 0 ? b.w : (b.w < pl.n_rows0 ? pl.rows[b.w].w : 0);
-        if (a.x != b.x || a.y != b.y || a.z != b.z || a.w != bw) return fail("slot record", slot, i);
+        const int st = d[D_CODE] >> 4;
+        const I4 e = st == 0 ? I4{b.y, b.z, b.x, bw} : st == 1 ? I4{b.x, b.z, b.y, bw} : I4{b.x, b.y, b.z, bw};
+        if (a.x != e.x || a.y != e.y || a.z != e.z || a.w != e.w) return fail("slot record", slot, i);
         if (g == 1 && b.w < pl.n_rows0 && bw <= 0) return fail("slot count", slot, i);
       }
     }
@@ -121,7 +124,10 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
         if (t < 0) continue;
         if (t >= pl.sk_slots[1] * 4 * Lb) return fail("urow12 range", i, t);
         const I4& b = pl.sk_urec[1][t];
-        if (a.x != b.x || a.y != b.y || a.z != b.z || a.w <= 0) return fail("urow12 target", i, t);
+        // the same triple (stream 0 holds (j, k, i), streams 1 / 2 (i, k, j) / (i, j, k)) and count
+        const int ti = a.z, tj = a.x, tk = a.y;
+        const bool same = (b.x == ti && ((b.y == tk && b.z == tj) || (b.y == tj && b.z == tk)));
+        if (!same || a.w <= 0 || b.w != a.w) return fail("urow12 target", i, t);
       }
     }
   }
@@ -157,7 +163,8 @@ int main() {
       const int* d = &pl.udesc[(size_t)u * UD];
       const int* dn = &pl.udesc[(size_t)(u + 1) * UD];
       if (dn[D_CODE] != d[D_CODE]) continue;  // the section's last unit
-      if (d[D_END] - d[0] != LCAP_SK && d[D_NST] != pl.gu) return fail("fill", (int)u, d[D_END] - d[0]);
+      const int lm = pl.lmax[(d[D_CODE] >> 4) == 0 ? 0 : 1];
+      if (d[D_END] - d[0] != lm && d[D_NST] != pl.gu) return fail("fill", (int)u, d[D_END] - d[0]);
     }
   }
 

@@ -412,11 +412,16 @@ def test_in_place_link_edit_between_iterations_matches_oracle():
 
 
 @pytest.mark.parametrize("K,env", [(10, {}), (10, {"MMSBM_SK": "0"}), (12, {"MMSBM_UNITS": "1,1"}),
-                                   (7, {"MMSBM_UNITS": "5,9"}), (13, {})])
+                                   (7, {"MMSBM_UNITS": "5,9"}), (13, {}),
+                                   (10, {"MMSBM_SK_FUSED": "0"}), (11, {"MMSBM_SK_FUSED": "0"}),
+                                   (9, {"MMSBM_SK_FUSED": "0", "MMSBM_UNITS": "7,3"}),
+                                   (10, {"MMSBM_UNITS": "1,1"}), (5, {"MMSBM_UNITS": "40,40"})])
 def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
-    """K <= 12 runs the small-K kernels (csrc/sk.h), K > 12 the large-K ones; MMSBM_SK=0 forces the
-    large-K family at K=10, MMSBM_UNITS forces long (16-chunk) or short units.  Every variant
-    matches the C oracle (2 iterations, train and held-out likelihood)."""
+    """K <= 12 runs the small-K kernels (csrc/sk.h; the fused E-step by default, pass A + pass B
+    with MMSBM_SK_FUSED=0; 8 stretches per unit at K <= 10, 4 above), K > 12 the large-K ones;
+    MMSBM_SK=0 forces the large-K family at K=10, MMSBM_UNITS forces long (up to 128 chunks: eight
+    16-chunk blocks per unit) or short units.  Every variant matches the C oracle (2 iterations,
+    train and held-out likelihood)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     tr, te = _fold(tmp_path, 400, 12000, seed=31 + K, multi_frac=0.1, both_frac=0.03)
@@ -426,7 +431,10 @@ def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
     theta0, pr0 = np.array(m.theta), np.array(m.pr)
     m.make_iterations(2)
     info = m._engine.plan_info()
-    assert info["small_k"] == (1 if K <= 12 and env.get("MMSBM_SK") != "0" else 0)
+    small = K <= 12 and env.get("MMSBM_SK") != "0"
+    assert info["small_k"] == (0 if not small else 1 if env.get("MMSBM_SK_FUSED") == "0" else 2)
+    if small:
+        assert info["genes_per_wg_max"] == (8 if K <= 10 else 4)
     th_o, pr_o, L_o, LT_o = _oracle_run(m, theta0, pr0, 2)
     np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)

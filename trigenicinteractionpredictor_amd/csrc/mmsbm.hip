@@ -1675,7 +1675,13 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   // unit counts do not depend on B, so a sample's sums (and its bits) are the same whatever its
   // batch; MMSBM_UNITS="a,b" overrides them (tests: tiny units force every split path).  The fused
   // small-K launch packs full units (as few as the chunk cap allows: the grid must be resident).
-  int units_a = c->sk_fused ? 1 : 1536, units_b = c->sk_fused ? 1 : 3072;
+  int units_a = 1536, units_b = 3072;
+  if (c->sk_fused) {  // about the waves resident at once: 15 per CU (two 8-wave workgroups, some
+    int ncu = 0;      // headroom for units the stretch cap or a section's end leave short)
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu < 1)
+      ncu = 256;
+    units_a = units_b = 15 * ncu;
+  }
   if (const char* u = getenv("MMSBM_UNITS")) {
     int a = 0, b = 0;
     if (sscanf(u, "%d,%d", &a, &b) == 2 && a > 0 && b > 0) {
@@ -2002,7 +2008,7 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[9] = h.prow_ptr.empty() ? 0 : h.prow_ptr[(size_t)h.R * (h.P + 1)];  // stream-0 partial rows
   info[7] = h.small ? h.gu : h.gmax;
   info[8] = h.small ? info[9] : (int64_t)h.vgenes.size();  // small-K: one V table per stream-0 stretch
-  info[10] = h.small ? 1 : 0;
+  info[10] = h.small ? (c->sk_fused ? 2 : 1) : 0;
   info[11] = h.small ? h.n_units : (int64_t)(h.n_wg_a + h.n_wg_b) * NW;
   return MMSBM_OK;
 }

@@ -28,10 +28,11 @@ constexpr int CH = 4;   // observations per chunk (one MFMA k-step)
 constexpr int NW = 8;   // waves (units) per workgroup
 // Small-K plans (K <= 12, the register-direct kernels of sk.h): a unit has at most `gu` <= GU gene
 // stretches (one wave keeps their V tables and M rows, and contracts them with p at its end; gu is
-// the kernel's LDS budget: 8 at K <= 10, 4 above) and at most LCAP_SK chunks (its records are staged
-// in the wave's LDS at once).
+// the kernel's LDS budget: 8 at K <= 10, 4 above) and at most LCAP_SK chunks, processed in blocks of
+// SK_BLOCK chunks (one block's records are staged in the wave's LDS at a time).
 constexpr int GU = 8;
-constexpr int LCAP_SK = 16;
+constexpr int SK_BLOCK = 16;
+constexpr int LCAP_SK = 128;
 // unit descriptor: stretch start chunks [0, GU) (unused ones = the end), end chunk [D_END], stretches
 // [D_NST], partial rows [D_PROW, +GU), pivot genes [D_GENE, +GU), stream * 16 + rating [D_CODE]
 constexpr int D_END = GU, D_NST = GU + 1, D_PROW = GU + 2, D_GENE = 2 * GU + 2, D_CODE = 3 * GU + 2;
@@ -73,6 +74,7 @@ struct Plan {
   // major, then wave); a slot holds one unit or nothing.  Records are copied slot-major with a fixed
   // capacity of 4 L rows per slot, so a wave finds its unit's records from its slot number alone.
   int sk_L[2] = {0, 0};            // chunks per slot (the group's longest unit)
+  int lmax[2] = {0, 0};            // the unit length the packing aimed at (stream 0, streams 1 / 2)
   long long sk_slots[2] = {0, 0};
   std::vector<int> sk_udesc[2];    // [slots][UD]: unit descriptors with the stretch starts and end
                                    // relative to the slot's first chunk (D_NST 0: empty slot)
@@ -166,10 +168,13 @@ inline void make_slots(Plan& pl) {
         const long long row0 = 4LL * c0, nrow = 4LL * (d[D_END] - c0);
         for (long long i = 0; i < 4LL * L; ++i) {
           const long long row = row0 + (i < nrow ? i : nrow - 1);  // padding: the unit's last row
-          rec[i] = pl.rows[row];
-          // streams 1, 2: the observation's count n (its stream-0 row's w; 0 on padding rows), for
-          // the fused kernel that computes c itself (pass B reads c by position and ignores w)
-          if (g == 1) rec[i].w = rec[i].w < pl.n_rows0 ? pl.rows[rec[i].w].w : 0;
+          // (u gene, v gene, pivot gene, n) in the slot's stream order: stream 0 (j, k, i),
+          // stream 1 (i, k, j), stream 2 (i, j, k); n = the count (streams 1, 2: the stream-0 row's
+          // w, 0 on padding rows; pass B reads c by position and ignores it)
+          const I4 x = pl.rows[row];
+          const int st = pl.wg_code[w] >> 4;
+          const int n = g == 0 ? x.w : (x.w < pl.n_rows0 ? pl.rows[x.w].w : 0);
+          rec[i] = st == 0 ? I4{x.y, x.z, x.x, n} : st == 1 ? I4{x.x, x.z, x.y, n} : I4{x.x, x.y, x.z, n};
           if (i < nrow) pos[row] = slot * 4 * L + i;
         }
       }
@@ -241,10 +246,18 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
     }
   // unit length: the work spread over about units_* units, but no unit longer than LCAP chunks
   // (large link sets get more units rather than longer ones, so a few long units do not set
-  // the kernel's duration)
+  // the kernel's duration).  Fill-packed small plans (the fused launch) take units_a as the
+  // number of units for all streams together (about the waves that are resident at once) and
+  // one length for every stream, at least one block.
   const long long LCAP = small ? LCAP_SK : 64;
-  const int lmax_a = (int)std::min(LCAP, std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1)));
-  const int lmax_b = (int)std::min(LCAP, std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1)));
+  int lmax_a = (int)std::min(LCAP, std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1)));
+  int lmax_b = (int)std::min(LCAP, std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1)));
+  if (small && fill) {
+    const long long all = chunks_a + chunks_b;
+    lmax_a = lmax_b = (int)std::min(LCAP, std::max<long long>(SK_BLOCK, (all + units_a - 1) / std::max(units_a, 1)));
+  }
+  pl.lmax[0] = lmax_a;
+  pl.lmax[1] = lmax_b;
   if (small) {  // one unit per wave: rounds stay 1 (wg_target is kept for the plan checker)
     pl.rounds_a = pl.rounds_b = 1;
     (void)wg_target;

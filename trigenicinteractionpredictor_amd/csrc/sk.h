@@ -32,10 +32,13 @@
 // s summed against theta_g), so nothing waits for another workgroup: pass A's c stores, pass B's c
 // loads and one dependent launch per iteration go away for 2x the Z / d / c work.
 enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
+#ifndef MMSBM_SK_PAIR
+#define MMSBM_SK_PAIR 0  // phase 1 one chunk per round (1: rounds of two, measured slower)
+#endif
 
-constexpr int LC = mmsbm_plan::LCAP_SK;           // most chunks of one unit (gathered at once)
-constexpr int SK_ROWS = 4 * mmsbm_plan::LCAP_SK;  // records staged per wave (one unit)
-constexpr int RPL = (SK_ROWS + 63) / 64;          // staged records per lane
+constexpr int LC = mmsbm_plan::SK_BLOCK;          // chunks of one block (gathered at once)
+constexpr int SK_ROWS = 4 * mmsbm_plan::SK_BLOCK;  // records staged per wave (one block, one per lane)
+static_assert(SK_ROWS == 64, "one record per lane");
 
 template <int K>
 struct SKT {
@@ -46,13 +49,15 @@ struct SKT {
   static constexpr int SLOT = 4 * NCT;            // doubles per stretch slot (V table, then M row)
   // P^s_r staged per workgroup, plain [z][cell] order, zero past K^3 up to the last word the
   // unguarded V-operand reads touch (rows a >= K of the 4-wide a tiles, cells up to 16 NCG)
-  static constexpr int PVR = (4 * NG - 1) * K2 + 16 * NCG;
+  static constexpr int PVR = (K - 1) * K2 + 16 * NCG;  // (V-operand rows a >= K read row K - 1)
   static constexpr int PSD = ((PVR > K3 ? PVR : K3) + 1) & ~1;
   static constexpr int GUK = mmsbm_plan::sk_gu(K);  // stretches per unit (slots per wave): 8 or 4
   static constexpr int NT2 = GUK / 4;                // 4-row MFMA tiles of the unit's stretches
-  static constexpr int WAVE = GUK * SLOT + 2 * SK_ROWS + SK_ROWS + 64 + SK_ROWS;  // slots,
-                                                             // records, aux, transpose, d / c words
-  static constexpr int WAVE_B = WAVE - 64 - SK_ROWS;  // pass B: c arrives in aux
+  static constexpr int THL = GUK * 4 * NG;          // the unit's pivot-gene theta rows (S operand)
+  // per wave: slots, the block's (u, v) gene pairs, pivot rows, aux (row12 / c), two transposes,
+  // d / c words
+  static constexpr int WAVE = GUK * SLOT + SK_ROWS + THL + SK_ROWS + 2 * 64 + SK_ROWS;
+  static constexpr int WAVE_B = WAVE - 2 * 64 - SK_ROWS;  // pass B: c arrives in aux
   static constexpr int LDS_B = (PSD + NW * WAVE_B) * 8;
   static constexpr int WAVE_U = WAVE - SK_ROWS;   // fused: no row12 / c staging
   static constexpr int NPV = (PSD + NT - 1) / NT; // staged words per thread
@@ -64,12 +69,12 @@ struct SKT {
   static_assert(LDS_U <= 80 * 1024, "two fused / likelihood workgroups per CU");
   static_assert(LDS <= 160 * 1024, "pass A LDS");
   static_assert(GUK % 4 == 0 && GUK <= mmsbm_plan::GU, "stretch tiles");
-  static_assert(GUK * 4 * NG <= 2 * SK_ROWS, "pivot-gene theta rows over the records");
+
   static_assert(SLOT >= 4 * NCT, "slot holds a V table / M row");
   // the unguarded V / M reads stay inside the slots and the records (finite words)
-  static_assert((GUK - 1) * SLOT + 15 * K + 4 * NG <= GUK * SLOT + 2 * SK_ROWS,
+  static_assert((GUK - 1) * SLOT + 15 * K + 4 * NG <= GUK * SLOT + SK_ROWS + THL,
                 "V reads past the wave's slots and records");
-  static_assert(16 * NCG <= SLOT + 2 * SK_ROWS, "S operand reads past the slots and records");
+  static_assert(16 * NCG <= SLOT + SK_ROWS + THL, "S operand reads past the slots and records");
 };
 
 // n / d by v_rcp_f64 and two Newton steps plus a residual correction (within an ulp or two of the
@@ -98,8 +103,8 @@ struct SkSec {  // workgroup sections of a small-K plan (Plan::sk_wg_end)
 // streams 1 and 2; SK_U: both groups, group 0's n_wg workgroups first, then group 1's (urec1,
 // udesc1, L1).  Wave wv of workgroup w of a group owns unit slot w NW + wv (Plan::sk_*).
 template <int K, int MODE>
-// (pass B: 6 waves per SIMD = three workgroups per CU, which its LDS allows)
-__global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
+// (4 waves per SIMD: two workgroups per CU, the LDS budget of the fused launch)
+__global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     const int4* __restrict__ urec, const int* __restrict__ udesc, const int2* __restrict__ urow12,
     const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ cB,
     double* __restrict__ xpart, double* __restrict__ spart, double* __restrict__ partL, SkSec sec,
@@ -130,10 +135,11 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
   double* wl = smem + T::PSD + wv * (MODE == SK_B ? T::WAVE_B : MODE == SK_U ? T::WAVE_U : T::WAVE);
   constexpr int GUK = T::GUK, NT2 = T::NT2;
   double* MSl = wl;                                                 // GUK slots: V, then M
-  int4* REC = reinterpret_cast<int4*>(wl + GUK * SLOT);             // the unit's records
-  double* AUX = wl + GUK * SLOT + 2 * SK_ROWS;                      // row12 (A) / c (B)
+  int2* REC = reinterpret_cast<int2*>(wl + GUK * SLOT);             // the block's (u, v) genes
+  double* THl = wl + GUK * SLOT + SK_ROWS;                          // pivot theta rows [GUK][4 NG]
+  double* AUX = THl + T::THL;                                       // row12 (A) / c (B)
   double* TRl = MODE == SK_U ? AUX : AUX + SK_ROWS;                 // Z operand transpose
-  double* DL = TRl + 64;                                            // d, then c, per observation
+  double* DL = TRl + 2 * 64;                                        // d, then c, per observation
   double* __restrict__ cBb = cB + (size_t)b * n_cb;
   double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
   Stamp st_{};
@@ -154,16 +160,34 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
     pvv[i] = ok ? v : 0.0;
   }
 
-  // One slot's descriptor, records (+ row12 / c) and pivot-gene theta, loaded together.
+  // One slot's descriptor and pivot-gene theta, with its first block's records (+ row12 / c).
+  // A unit of c1 chunks runs in blocks of LC chunks (SK_ROWS records, one per lane); the next
+  // block's records are loaded while the current one computes.
+  const long long slot = (long long)w * NW + wv;
   struct Unit {
     int nst, c1, ds[GUK], prow[NT2];
-    int4 rv[RPL];
-    int2 r12[RPL];
-    double cv[RPL];
     double tv[NT2][NG];     // theta_{gene 4 tt + lo}[4 as + hi] (A of V; zero past nst and K)
   };
+  struct Blk {
+    int4 rv;
+    int2 r12;
+    double cv;
+  };
+  auto load_block = [&](int bi, Blk& bk) {  // (rows past the slot's capacity: its last, valid row)
+    const int idx = SK_ROWS * bi + lane;
+    const long long row = slot * 4 * L + (idx < 4 * L ? idx : 4 * L - 1);
+    bk.rv = urec[row];
+    if constexpr (MODE == SK_A) bk.r12 = urow12[row];
+    if constexpr (MODE == SK_B) bk.cv = cBb[row];
+  };
+  int wlane = 0;  // the count n of this lane's observation in the current block
+  auto stage_block = [&](const Blk& bk) {
+    REC[lane] = make_int2(bk.rv.x, bk.rv.y);
+    wlane = bk.rv.w;
+    if constexpr (MODE == SK_A) reinterpret_cast<int2*>(AUX)[lane] = bk.r12;
+    if constexpr (MODE == SK_B) AUX[lane] = bk.cv;
+  };
   auto load_unit = [&](Unit& un) {
-    const long long slot = (long long)w * NW + wv;
     const int* __restrict__ d = udesc + slot * mmsbm_plan::UD;
     un.nst = __builtin_amdgcn_readfirstlane(d[mmsbm_plan::D_NST]);  // wave-uniform (scalar control flow)
     un.c1 = __builtin_amdgcn_readfirstlane(d[mmsbm_plan::D_END]);
@@ -171,17 +195,6 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
     for (int t = 0; t < GUK; ++t) un.ds[t] = __builtin_amdgcn_readfirstlane(d[t]);
 #pragma unroll
     for (int tt = 0; tt < NT2; ++tt) un.prow[tt] = d[mmsbm_plan::D_PROW + 4 * tt + hi];
-    const int nrow = 4 * L;  // the slot's capacity (every row valid: make_slots pads), so the record
-                             // loads do not wait for the descriptor
-    const long long rbase = slot * 4 * L;
-#pragma unroll
-    for (int i = 0; i < RPL; ++i) {
-      const int idx = lane + 64 * i;
-      const long long row = rbase + (idx < nrow ? idx : nrow - 1);
-      un.rv[i] = urec[row];
-      if constexpr (MODE == SK_A) un.r12[i] = urow12[row];
-      if constexpr (MODE == SK_B) un.cv[i] = cBb[row];
-    }
     if constexpr (MODE != SK_B) {
 #pragma unroll
       for (int tt = 0; tt < NT2; ++tt) {
@@ -195,20 +208,15 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
       }
     }
   };
+  Blk bk;
+  load_block(0, bk);  // (the block loads do not wait for the descriptor)
   Unit un;
   load_unit(un);
 
 #pragma unroll
   for (int i = 0; i < T::NPV; ++i)
     if (tid + NT * i < T::PSD) PV[tid + NT * i] = pvv[i];
-  // the unit's records (and row12 / c) into this wave's LDS
-#pragma unroll
-  for (int i = 0; i < RPL; ++i) {
-    const int idx = lane + 64 * i;
-    REC[idx] = un.rv[i];
-    if constexpr (MODE == SK_A) reinterpret_cast<int2*>(AUX)[idx] = un.r12[i];
-    if constexpr (MODE == SK_B) AUX[idx] = un.cv[i];
-  }
+  stage_block(bk);  // the first block's records (and row12 / c) into this wave's LDS
   // pass B reads P^s only in the X contraction, behind the barrier after its chunk loop; the
   // passes that form V tables publish it here
   if constexpr (MODE == SK_B) wave_lds_sync();
@@ -238,39 +246,18 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
         if (t + 1 == i && i < nst) e = ds[i];
       return e;
     };
-    // ---- theta gathers.  Every theta value the unit needs is gathered at once, straight into the
-    // registers of the MFMA operands (lane (obs hi, col): theta_u and theta_v of its observation,
-    // column col), before the V tables are formed, so the round trip overlaps that work.  Columns
-    // col >= K are zeroed where a product needs it (the Z operand and d), at their first use, so no
-    // select waits for a load here.
-    const int4* __restrict__ rec = REC;
+    const int2* __restrict__ rec = REC;
     const int colc = col < K ? col : K - 1;
+    const unsigned cb = (unsigned)colc * 8u;
     const bool kcol = col < K;
     const double km = kcol ? 1.0 : 0.0;
-    double ga[LC], gv[LC];
-    auto gather = [&](int i) {
-      ga[i] = 0.0;  // (chunks past the unit's end stay zero)
-      gv[i] = 0.0;
-      if (i < c1) {  // uniform guard: a short unit issues only its own loads
-        const int4 rh = rec[i * 4 + hi];
-        const int gu = s == 0 ? rh.y : rh.x;   // u slot: j on stream 0, i on streams 1 / 2
-        const int gw = s == 2 ? rh.y : rh.z;   // v slot: k, except j on stream 2
-        ga[i] = th[(unsigned)(gu * K + colc)];  // (col >= K: a finite copy of column K - 1)
-        gv[i] = th[(unsigned)(gw * K + colc)];
-      }
-    };
-#pragma unroll
-    for (int i = 0; i < LC; ++i) gather(i);
-    const int wlane = rec[lane].w;  // this lane's observation's count (the records die here)
-    // the unit's pivot-gene theta rows, [GUK][4 NG] words over the records (read in order after
-    // them: a wave's LDS operations complete in order), the S contraction's A operand
-    double* THl = reinterpret_cast<double*>(REC);
     const auto& tv = un.tv;  // (array references: the indices stay compile-time constants)
     if constexpr (MODE != SK_B) {
       // ---- V_g[cell] = sum_a theta_g[a] P^s[a][cell] for the unit's genes (m = gene, k = a, B
       // from the staged lattice: rows a >= K meet zero theta, words past K^3 are zero), into slot g
       // of the wave's LDS (cell = b K + h).  Every word of the GU slots is written (zero past K^2
-      // and for absent stretches), so the unguarded V / M reads below see finite values.
+      // and for absent stretches), so the unguarded V / M reads below see finite values.  The
+      // unit's pivot theta rows go to THl (the S contraction's A operand).
 #pragma unroll
       for (int tt = 0; tt < NT2; ++tt) {
         const bool live = tt == 0 || nst > 4 * tt;  // (uniform) a tile without stretches: zeros
@@ -280,97 +267,152 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
           double v = 0.0;
           if (live) {
 #pragma unroll
-            for (int as = 0; as < NG; ++as) v = mfma4(tv[tt][as], PV[(4 * as + hi) * K2 + cell], v);
+            for (int as = 0; as < NG; ++as)  // (rows a >= K: zero theta times row K - 1)
+              v = mfma4(tv[tt][as], PV[(4 * as + hi < K ? 4 * as + hi : K - 1) * K2 + cell], v);
           }
           if (cell < SLOT) MSl[(4 * tt + hi) * SLOT + cell] = cell < K2 ? v : 0.0;
         }
 #pragma unroll
         for (int as = 0; as < NG; ++as)
           if (blk == 0) THl[(4 * tt + lo) * 4 * NG + 4 * as + hi] = tv[tt][as];
-        // (one tile's operand reads in flight at a time: beside the LC chunks' gathers, both tiles'
-        // would not fit the register budget)
-        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);  // (one tile's operand reads in flight at a time)
       }
     } else {
       // pass B forms no V tables: the slots' words past each M row stay finite (zero)
 #pragma unroll
       for (int i = 0; i < (GUK * SLOT + 63) / 64; ++i)
         if (lane + 64 * i < GUK * SLOT) MSl[lane + 64 * i] = 0.0;
+#pragma unroll
+      for (int i = 0; i < (T::THL + 63) / 64; ++i)
+        if (lane + 64 * i < T::THL) THl[lane + 64 * i] = 0.0;
     }
     wave_lds_sync();
     st_.mark(1);
 
-    if constexpr (MODE != SK_B) {
-      // ---- d of every observation of the unit.  Per chunk: Z[obs hi][b = col] =
-      // sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA (A = theta_v(obs lo)[4 hs + hi], the transpose of
-      // the gathered tile, through the wave's LDS), d = eps + sum_b theta_u[b] Z[b] by a DPP row sum;
-      // d is parked at DL[4 q + obs] (one word per observation = per lane of the wave).
-      double vb[NG];  // B of Z: V_t[b = col][h = 4 hs + hi] (unguarded: zero A columns cancel h >= K)
-      auto load_v = [&](int t) {
+    const double* __restrict__ vrow = MSl + col * K + hi;
+    const double* __restrict__ cw = MODE == SK_B ? AUX : DL;
+    d4v m16 = d4v{0.0, 0.0, 0.0, 0.0};  // the running stretch's M (persists across blocks)
+    int t = 0;
+    int send = stretch_end(0);
+    double vb[NG];  // B of Z: V_vt[b = col][h = 4 hs + hi] of the running stretch (phase 1)
+    auto load_v = [&](int tv_) {
 #pragma unroll
-        for (int hs = 0; hs < NG; ++hs) vb[hs] = MSl[t * SLOT + col * K + 4 * hs + hi];
-      };
-      int t = 0;
-      int send = stretch_end(0);
-      load_v(0);
+      for (int hs = 0; hs < NG; ++hs) vb[hs] = vrow[tv_ * SLOT + 4 * hs];
+    };
+    int vt = 0, vsend = send;
+    if constexpr (MODE != SK_B) load_v(0);
+    for (int b0 = 0; b0 < c1; b0 += LC) {  // (uniform; one block for units of <= LC chunks)
+      const int nb = c1 - b0;               // chunks left (this block: min(nb, LC))
+      if (b0 > 0) {  // this block's records (loaded during the last one) into the wave's LDS
+        wave_lds_sync();
+        stage_block(bk);
+        wave_lds_sync();
+      }
+      if (nb > LC) load_block(b0 / LC + 1, bk);  // the next block's records, in flight meanwhile
+      // ---- theta gathers: every value of the block at once, straight into the registers of the
+      // MFMA operands (lane (obs hi, col): theta_u and theta_v of its observation, column col);
+      // columns col >= K are zeroed where a product needs it (the Z operand and d), at first use,
+      // so no select waits for a load here
+      double ga[LC], gv[LC];
 #pragma unroll
-      for (int q = 0; q < LC; ++q) {
-        if (q < c1) {  // (a guard, not a break: the loop keeps one exit and unrolls fully)
-          TRl[lane] = gv[q] * km;
-          wave_lds_sync();
-          double z = 0.0;
-#pragma unroll
-          for (int hs = 0; hs < NG; ++hs) z = mfma4(TRl[16 * lo + 4 * hs + hi], vb[hs], z);
-          const double dd = row16_sum(ga[q] * km * z) + eps;
-          if (col == 0) DL[q * 4 + hi] = dd;
-          if (q + 1 == send) {
-            ++t;
-            send = stretch_end(t);
-            if (t < nst) load_v(t);
-          }
+      for (int i = 0; i < LC; ++i) {
+        ga[i] = 0.0;  // (chunks past the unit's end stay zero)
+        gv[i] = 0.0;
+        if (i < nb) {  // uniform guard: a short block issues only its own loads
+          const int2 rh = rec[i * 4 + hi];  // (u gene, v gene): make_slots orders them
+          // (32-bit byte offsets from the sample's theta base: one 24-bit multiply-add per address;
+          // col >= K reads a finite copy of column K - 1)
+          const char* __restrict__ thb = reinterpret_cast<const char*>(th);
+          ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
+          gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
         }
       }
-      wave_lds_sync();
-      // ---- one observation per lane: c = n / d (or n log d), once per observation instead of
-      // once per 16 lanes of it
-      const double dl = DL[lane];
-      const double wn = (double)wlane;
-      const bool real = lane < 4 * c1;
-      if constexpr (MODE == SK_LL) {
-        if (real) ll = wn * log(dl);
-      } else {
-        const double cl = sk_div(wn, dl);
-        DL[lane] = cl;
-        if (MODE == SK_A && real) {
-          const int2 rr = reinterpret_cast<const int2*>(AUX)[lane];
-          if (rr.x >= 0) {
-            cBb[rr.x] = cl;
-            cBb[rr.y] = cl;
-          }
-        }
-      }
-      wave_lds_sync();
-    }
-    if constexpr (MODE != SK_LL) {
-      // ---- M^s += c theta_u (x) theta_v over each chunk's 4 observations (k = observation), c
-      // broadcast from the observation's word; a stretch's M row replaces its V table in slot t
-      const double* __restrict__ cw = MODE == SK_B ? AUX : DL;
-      d4v m16 = d4v{0.0, 0.0, 0.0, 0.0};
-      int t = 0;
-      int send = stretch_end(0);
+      if constexpr (MODE != SK_B) {
+        // ---- d of every observation of the block, two chunks per round (their latency chains
+        // interleave).  Per chunk: Z[obs hi][b = col] = sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA
+        // (A = theta_v(obs lo)[4 hs + hi], the transpose of the gathered tile, through the wave's
+        // LDS; B unguarded: zero A columns cancel h >= K), d = eps + sum_b theta_u[b] Z[b] by a DPP
+        // row sum; d is parked at DL[4 q + obs] (one word per observation = per lane of the wave;
+        // the 16 lanes of a row hold the same bits and store the same word).  Chunk q's V table is
+        // slot t(q) = #{stretch starts <= q} (unused starts sit at the unit's end); a chunk past
+        // the end has zero theta (d = eps, never used).
+#if MMSBM_SK_PAIR == 0
 #pragma unroll
-      for (int q = 0; q < LC; ++q) {
-        if (q < c1) {
-          m16 = mfma16(ga[q], cw[q * 4 + hi] * gv[q], m16);
-          if (q + 1 == send) {  // stretch t done: its M row into slot t
+        for (int q = 0; q < LC; ++q) {
+          if (q < nb) {
+            TRl[lane] = gv[q] * km;
+            wave_lds_sync();
+            double z = 0.0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int x = hi + 4 * i;
-              if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
+            for (int hs = 0; hs < NG; ++hs) z = mfma4(TRl[16 * lo + 4 * hs + hi], vb[hs], z);
+            DL[q * 4 + hi] = row16_sum(ga[q] * km * z) + eps;
+            if (b0 + q + 1 == vsend) {  // the next stretch's V operand
+              ++vt;
+              vsend = stretch_end(vt);
+              if (vt < nst) load_v(vt);
             }
-            m16 = d4v{0.0, 0.0, 0.0, 0.0};
-            ++t;
-            send = stretch_end(t);
+          }
+        }
+#else  // (measured slower: rounds of two chunks, the V operand read per chunk)
+#pragma unroll
+        for (int q0 = 0; q0 < LC; q0 += 2) {
+          if (q0 < nb) {  // (a guard, not a break: the loop keeps one exit and unrolls fully)
+            TRl[lane] = gv[q0] * km;
+            TRl[64 + lane] = gv[q0 + 1] * km;
+            wave_lds_sync();
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int q = q0 + u, qa = b0 + q;
+              int tq = 0;
+#pragma unroll
+              for (int i = 1; i < GUK; ++i) tq += ds[i] <= qa ? 1 : 0;
+              double z = 0.0;
+#pragma unroll
+              for (int hs = 0; hs < NG; ++hs)
+                z = mfma4(TRl[64 * u + 16 * lo + 4 * hs + hi], vrow[tq * SLOT + 4 * hs], z);
+              DL[q * 4 + hi] = row16_sum(ga[q] * km * z) + eps;
+            }
+          }
+        }
+#endif
+        wave_lds_sync();
+        // ---- one observation per lane: c = n / d (or n log d), once per observation instead of
+        // once per 16 lanes of it
+        const double dl = DL[lane];
+        const double wn = (double)wlane;
+        const bool real = lane < 4 * nb;
+        if constexpr (MODE == SK_LL) {
+          if (real) ll += wn * log(dl);
+        } else {
+          const double cl = sk_div(wn, dl);
+          DL[lane] = cl;
+          if (MODE == SK_A && real) {
+            const int2 rr = reinterpret_cast<const int2*>(AUX)[lane];
+            if (rr.x >= 0) {
+              cBb[rr.x] = cl;
+              cBb[rr.y] = cl;
+            }
+          }
+        }
+        wave_lds_sync();
+      }
+      if constexpr (MODE != SK_LL) {
+        // ---- M^s += c theta_u (x) theta_v over each chunk's 4 observations (k = observation), c
+        // broadcast from the observation's word; a stretch's M row replaces its V table in slot t
+#pragma unroll
+        for (int q = 0; q < LC; ++q) {
+          if (q < nb) {
+            m16 = mfma16(ga[q], cw[q * 4 + hi] * gv[q], m16);
+            if (b0 + q + 1 == send) {  // stretch t done: its M row into slot t
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int x = hi + 4 * i;
+                if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
+              }
+              m16 = d4v{0.0, 0.0, 0.0, 0.0};
+              ++t;
+              send = stretch_end(t);
+            }
           }
         }
       }
@@ -380,7 +422,6 @@ __global__ __launch_bounds__(NT, MODE == SK_B ? 6 : 4) void sk_pass_kernel(
   if constexpr (MODE != SK_LL) __syncthreads();  // every wave's share of P^s staged
   if (un.nst > 0) {
     const int nst = un.nst;
-    const double* THl = reinterpret_cast<const double*>(REC);  // (see the unit prologue)
     if constexpr (MODE != SK_LL) {
       // ---- X_q[z] = sum_cell P^s[z][cell] M_q[cell] for the unit's rows q (m = q, n = z in the
       // block's z tile, k = 4 cells per step)
