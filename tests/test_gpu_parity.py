@@ -116,6 +116,25 @@ def test_against_c_oracle(tmp_path, K, P, E, iters):
     np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
 
 
+@pytest.mark.parametrize("hub", [(0.02, 0.3), (0.01, 0.6)])
+def test_hub_fold0_against_c_oracle(tmp_path, hub):
+    """A fold0-sized (P=1500, 90k triples) hub-heavy fold, shaped like get_input's trigenic screens
+    (:218-318: a few query genes in many triples; data.FoldSpec.hub_*): hub genes' pivot runs span
+    many units and blocks.  K=10 (the headline kernels) vs the C oracle, 2 iterations."""
+    tr, te = _fold(tmp_path, 1500, 90000, seed=77, multi_frac=0.05, both_frac=0.02,
+                   hub_frac=hub[0], hub_share=hub[1])
+    m = _gpu_model(tr, te)
+    random.seed(5)
+    m.initialize_parameters(10)
+    theta0, pr0 = np.array(m.theta), np.array(m.pr)
+    m.make_iterations(2)
+    th_o, pr_o, L_o, LT_o = _oracle_run(m, theta0, pr0, 2)
+    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
+    np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
+
+
 @pytest.mark.parametrize("units", ["1,1", "3,5", None])
 @pytest.mark.parametrize("K", [3, 10, 16])
 def test_work_plan_splits_match_oracle(tmp_path, monkeypatch, K, units):

@@ -4,14 +4,17 @@ at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE, both in KiB per dispatch, averaged o
 of the PMC passes.  The record is stamped with the build id of the library the passes ran (the
 `build_id` field of the bench lines they printed, which must all agree): bench.py only reports a
 record whose build id equals its own library's.
-usage: python tools/pmc_to_traffic.py gpurun_out/<tag> K E_obs B out.json"""
+usage: python tools/pmc_to_traffic.py gpurun_out/<tag> K E_obs B out.json  (from tools/gpu_r03_prof.sh)"""
 import collections
 import csv
 import glob
 import json
 import sys
 
-NAMES = {"pass_kernel<%d, 0>": "pass_a", "pass_kernel<%d, 2>": "pass_b", "fin_kernel<%d, false>": "fin"}
+NAMES = {"pass_kernel<%d, 0>": "pass_a", "pass_kernel<%d, 2>": "pass_b", "fin_kernel<%d, false>": "fin",
+         # small-K kernels (csrc/sk.h): the fused E-step is the iteration's "pass_a"
+         "sk_pass_kernel<%d, 3>": "pass_a", "sk_pass_kernel<%d, 0>": "pass_a",
+         "sk_pass_kernel<%d, 2>": "pass_b", "sk_fin_kernel<%d, false>": "fin"}
 
 
 def main(root, K, E_obs, B, out):

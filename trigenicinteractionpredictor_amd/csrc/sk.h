@@ -546,7 +546,16 @@ __device__ __forceinline__ double sk_gene_sum(const double* __restrict__ xb, con
   for (int c = 0; c < NCC; ++c) {
     if (c < nc && qa[c] < qb[c]) {
       X += v1[c];
-      for (int q = qa[c] + 1; q < qb[c]; ++q) X += xb[(size_t)q * K + x];
+      // the rest of the combo's rows 8 loads at a time (a hub gene's pivot runs span many units),
+      // added in row order
+      for (int q = qa[c] + 1; q < qb[c]; q += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = xb[(size_t)(q + u < qb[c] ? q + u : q) * K + x];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (q + u < qb[c]) X += v[u];
+      }
     }
   }
   return X;
