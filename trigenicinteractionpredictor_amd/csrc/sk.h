@@ -32,8 +32,11 @@
 // s summed against theta_g), so nothing waits for another workgroup: pass A's c stores, pass B's c
 // loads and one dependent launch per iteration go away for 2x the Z / d / c work.
 enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
-#ifndef MMSBM_SK_PAIR
-#define MMSBM_SK_PAIR 0  // phase 1 one chunk per round (1: rounds of two, measured slower)
+#ifndef MMSBM_SK_TRSWZ
+#define MMSBM_SK_TRSWZ 1  // the Z operand transpose with a bank swizzle (r03u A/B: 38.5k vs 38.1k iter/s)
+#endif
+#ifndef MMSBM_SK_MRED
+#define MMSBM_SK_MRED 0  // 1: d's sum over b on MFMA, four chunks at a time (measured slower than the DPP row sum)
 #endif
 
 constexpr int LC = mmsbm_plan::SK_BLOCK;          // chunks of one block (gathered at once)
@@ -250,7 +253,6 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     const int colc = col < K ? col : K - 1;
     const unsigned cb = (unsigned)colc * 8u;
     const bool kcol = col < K;
-    const double km = kcol ? 1.0 : 0.0;
     const auto& tv = un.tv;  // (array references: the indices stay compile-time constants)
     if constexpr (MODE != SK_B) {
       // ---- V_g[cell] = sum_a theta_g[a] P^s[a][cell] for the unit's genes (m = gene, k = a, B
@@ -295,9 +297,12 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     int t = 0;
     int send = stretch_end(0);
     double vb[NG];  // B of Z: V_vt[b = col][h = 4 hs + hi] of the running stretch (phase 1)
-    auto load_v = [&](int tv_) {
+    auto load_v = [&](int tv_) {  // (zero for b = col >= K and h >= K: no mask on the products)
 #pragma unroll
-      for (int hs = 0; hs < NG; ++hs) vb[hs] = vrow[tv_ * SLOT + 4 * hs];
+      for (int hs = 0; hs < NG; ++hs) {
+        const double x = vrow[tv_ * SLOT + 4 * hs];
+        vb[hs] = kcol && 4 * hs + hi < K ? x : 0.0;
+      }
     };
     int vt = 0, vsend = send;
     if constexpr (MODE != SK_B) load_v(0);
@@ -328,49 +333,69 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
         }
       }
       if constexpr (MODE != SK_B) {
-        // ---- d of every observation of the block, two chunks per round (their latency chains
-        // interleave).  Per chunk: Z[obs hi][b = col] = sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA
-        // (A = theta_v(obs lo)[4 hs + hi], the transpose of the gathered tile, through the wave's
-        // LDS; B unguarded: zero A columns cancel h >= K), d = eps + sum_b theta_u[b] Z[b] by a DPP
-        // row sum; d is parked at DL[4 q + obs] (one word per observation = per lane of the wave;
-        // the 16 lanes of a row hold the same bits and store the same word).  Chunk q's V table is
-        // slot t(q) = #{stretch starts <= q} (unused starts sit at the unit's end); a chunk past
-        // the end has zero theta (d = eps, never used).
-#if MMSBM_SK_PAIR == 0
+        // ---- d of every observation of the block.  Per chunk: Z[obs hi][b = col] =
+        // sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA (A = theta_v(obs lo)[4 hs + hi], the transpose
+        // of the gathered tile, through the wave's LDS; B = the running stretch's V operand, zero for
+        // b >= K and h >= K), d = eps + sum_b theta_u[b] Z[b], parked at DL[4 q + obs] (one word per
+        // observation = per lane of the wave).  A chunk past the end has zero theta (never used).
+#if MMSBM_SK_MRED
+        // d of a group of 4 chunks: w_u[obs][col] = theta_u[col] Z[col] (zero for col >= K), then
+        // one v_mfma_f64_16x16x4 per chunk against a 0/1 selector, R += w_u E_u with
+        // E_u[k = obs][n] = [n == 4 u + obs], moves chunk u's observation obs to column n = 4 u + obs:
+        // lane (hi, n) receives the columns col = hi + 4 i (i = 0..3) of observation n; summed in
+        // the lane, then over the four rows by two lane swaps (xor 32, then 16: commutative, so
+        // every row gets the same bits).  d of (chunk 4 g + n / 4, obs n % 4) = DL[16 g + n].
+#pragma unroll
+        for (int g4 = 0; g4 < LC / 4; ++g4) {
+          if (4 * g4 < nb) {
+            d4v R = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int q = 4 * g4 + u;
+              TRl[lane] = gv[q];  // (h >= K: finite, against zero V)
+              wave_lds_sync();
+              double z = 0.0;
+#pragma unroll
+              for (int hs = 0; hs < NG; ++hs) z = mfma4(TRl[16 * lo + 4 * hs + hi], vb[hs], z);
+              R = mfma16(ga[q] * z, col == 4 * u + hi ? 1.0 : 0.0, R);
+              if (q < nb && b0 + q + 1 == vsend) {  // the next stretch's V operand
+                ++vt;
+                vsend = stretch_end(vt);
+                if (vt < nst) load_v(vt);
+              }
+            }
+            double sr = (R[0] + R[1]) + (R[2] + R[3]);
+            sr += __shfl_xor(sr, 32, 64);
+            sr += __shfl_xor(sr, 16, 64);
+            DL[16 * g4 + col] = sr + eps;
+          }
+        }
+#else  // d by a DPP row sum per chunk (r03s same-box A/B: 38.2k vs 37.4k iter/s with the MFMA sum)
 #pragma unroll
         for (int q = 0; q < LC; ++q) {
           if (q < nb) {
-            TRl[lane] = gv[q] * km;
+#if MMSBM_SK_TRSWZ  // column swizzle c ^ 4 (o >> 1): the reads of observations 0 / 2 (1 / 3) hit
+                    // different banks
+            TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = gv[q];
+            wave_lds_sync();
+            double z = 0.0;
+#pragma unroll
+            for (int hs = 0; hs < NG; ++hs)
+              z = mfma4(TRl[16 * lo + ((4 * hs + hi) ^ (4 * (lo >> 1)))], vb[hs], z);
+#else
+            TRl[lane] = gv[q];
             wave_lds_sync();
             double z = 0.0;
 #pragma unroll
             for (int hs = 0; hs < NG; ++hs) z = mfma4(TRl[16 * lo + 4 * hs + hi], vb[hs], z);
-            DL[q * 4 + hi] = row16_sum(ga[q] * km * z) + eps;
+#endif
+            // (the 16 lanes of a row hold the same bits and store the same word; storing from one
+            // lane per row measured no faster, r03u)
+            DL[q * 4 + hi] = row16_sum(ga[q] * z) + eps;
             if (b0 + q + 1 == vsend) {  // the next stretch's V operand
               ++vt;
               vsend = stretch_end(vt);
               if (vt < nst) load_v(vt);
-            }
-          }
-        }
-#else  // (measured slower: rounds of two chunks, the V operand read per chunk)
-#pragma unroll
-        for (int q0 = 0; q0 < LC; q0 += 2) {
-          if (q0 < nb) {  // (a guard, not a break: the loop keeps one exit and unrolls fully)
-            TRl[lane] = gv[q0] * km;
-            TRl[64 + lane] = gv[q0 + 1] * km;
-            wave_lds_sync();
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const int q = q0 + u, qa = b0 + q;
-              int tq = 0;
-#pragma unroll
-              for (int i = 1; i < GUK; ++i) tq += ds[i] <= qa ? 1 : 0;
-              double z = 0.0;
-#pragma unroll
-              for (int hs = 0; hs < NG; ++hs)
-                z = mfma4(TRl[64 * u + 16 * lo + 4 * hs + hi], vrow[tq * SLOT + 4 * hs], z);
-              DL[q * 4 + hi] = row16_sum(ga[q] * km * z) + eps;
             }
           }
         }
