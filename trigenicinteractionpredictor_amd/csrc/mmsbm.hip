@@ -616,6 +616,10 @@ struct SpRange {
 };
 
 template <int K>
+#ifndef MMSBM_FIN_PL
+#define MMSBM_FIN_PL 0  // 1: big fin with the combo's P^s in LDS where it fits (measured slower:
+                        // K=20 x 8 fin 266 vs 214 us, one workgroup per CU instead of two)
+#endif
 struct FT {
   static constexpr int K2 = K * K, NG = (K + 3) / 4, KP = 4 * NG;
   static constexpr int KS = (K2 + 3) / 4;       // k-steps over the dense (y, z) cells
@@ -634,16 +638,21 @@ struct FT {
                                      : (CB * 4 * K2P > 4 * NXG * 64 ? CB * 4 * K2P : 4 * NXG * 64);
   static constexpr int MS = MS_G > MAX_R * NPART * 64 ? MS_G : MAX_R * NPART * 64;  // doubles
   static constexpr bool PLDS = K <= 12;  // p of every rating staged in LDS (else read from L2)
+  // big fin (K > 12): the combo's P^s staged in LDS as [k][x] (x stride PLK) when it fits beside
+  // the gene rows (K <= 21), instead of each wave reading its p operands from L2
+  static constexpr int PLK = 4 * NG;
+  static constexpr int PLN = K2P * PLK;
+  static constexpr bool PLB = MMSBM_FIN_PL && GT > 1 && (MS + PLN) * 8 <= 160 * 1024;
   // cell part: CL rounds of 64 cells per workgroup (CL = 8 at K = 20 x 8 samples measured slower:
   // fin 221 -> 244 us, the longer cell workgroups finish last)
   static constexpr int CL = 1;
   static constexpr int NCW = (K * K * K + 64 * CL - 1) / (64 * CL);
-  static constexpr int LDS = (MS + (PLDS ? MAX_R * K * K * K : 0)) * 8;
+  static constexpr int LDS = (MS + (PLDS ? MAX_R * K * K * K : 0) + (PLB ? PLN : 0)) * 8;
   // big fin whose LDS lets two workgroups share a CU (K = 20-23): rounds of 6 partial-row entries
   // and a 128-VGPR budget (4 waves per SIMD; no spills there, K = 14-19 would spill 8-23); above,
   // LDS allows one workgroup and 12 entries per round keep more loads in flight
   static constexpr bool TWO = GT > 1 && 2 * LDS <= 160 * 1024 && K >= 20;
-  static constexpr int RE_CAP = TWO ? 6 : 12;
+  static constexpr int RE_CAP = (TWO || PLB) ? 6 : 12;  // (PLB: the staged P^s loads are live beside the round)
   static constexpr int WPE = TWO ? 4 : 1;
   static_assert(GT == 1 || NXG * KSPLIT == 8, "big fin: one (x group, k part) per wave");
   static_assert(GT == 1 || NGW * K <= NT, "big fin epilogue: one (gene, x) per thread");
@@ -704,6 +713,36 @@ __device__ __forceinline__ void x_tiles(const double* __restrict__ Mg, const dou
       else if constexpr (S == 2) idx = kc * K + xc;
       else idx = kc + (kc / K) * (K2 - K) + xc * K;
       bv[u] = p[idx];
+      kk[u] = k;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const bool ok = ks0 + u < ke;
+#pragma unroll
+      for (int t = 0; t < GT; ++t) {
+        const double m = Mg[t * 4 * F::K2P + kk[u]];
+        acc[t] = mfma4(ok ? m : 0.0, bv[u], acc[t]);
+      }
+    }
+  }
+}
+
+// x_tiles with the combo's P^s staged in LDS (FT::PLB): PL[k PLK + x], zero past K^2 and K.
+template <int K>
+__device__ __forceinline__ void x_tiles_pl(const double* __restrict__ Mg, const double* __restrict__ PL,
+                                           int x, int hi, int kb, int ke, double (&acc)[FT<K>::GT]) {
+  using F = FT<K>;
+  constexpr int UB = 8, GT = F::GT;
+  const int xc = x < K ? x : K - 1;
+#pragma unroll 1
+  for (int ks0 = kb; ks0 < ke; ks0 += UB) {
+    double bv[UB];
+    int kk[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int ks = ks0 + u < ke ? ks0 + u : ke - 1;
+      const int k = 4 * ks + hi;
+      bv[u] = PL[k * F::PLK + xc];
       kk[u] = k;
     }
 #pragma unroll
@@ -792,10 +831,31 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
   };
   __syncthreads();  // pp
   load_round(0, tid);
+  double* PL = Ms + F::MS;  // FT::PLB: the combo's P^s[k][x]
+  constexpr int NPL = (F::PLN + NT - 1) / NT;
   for (int combo = 0; combo < NC; ++combo) {
     __syncthreads();  // the previous combo's contraction is done with Ms
     st_.mark(4);
-    store_round(combo, tid);
+    if constexpr (F::PLB) {  // stage P^s of this combo: loads out first, stored after the rows
+      const int s = combo / R, r = combo % R;
+      const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
+      double pl[NPL];
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) {
+        const int e = tid + NT * i, k = e / F::PLK, xx = e % F::PLK;
+        const bool ok = e < F::PLN && k < K2 && xx < K;
+        const int kc = ok ? k : 0, xc = ok ? xx : 0;
+        const int idx = s == 0 ? xc * K2 + kc : s == 2 ? kc * K + xc : kc + (kc / K) * (K2 - K) + xc * K;
+        const double v = p[idx];
+        pl[i] = ok ? v : 0.0;
+      }
+      store_round(combo, tid);
+#pragma unroll
+      for (int i = 0; i < NPL; ++i)
+        if (tid + NT * i < F::PLN) PL[tid + NT * i] = pl[i];
+    } else {
+      store_round(combo, tid);
+    }
     for (int i0 = tid + RE * NT; i0 < NE; i0 += RE * NT) {
       load_round(combo, i0);
       store_round(combo, i0);
@@ -807,7 +867,8 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
     const int s = combo / R, r = combo % R;
     const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
     const double* __restrict__ Mg = Ms + (size_t)lo * F::K2P;
-    if (s == 0) x_tiles<K, 0>(Mg, p, x, hi, kb, ke, acc);
+    if constexpr (F::PLB) x_tiles_pl<K>(Mg, PL, x, hi, kb, ke, acc);
+    else if (s == 0) x_tiles<K, 0>(Mg, p, x, hi, kb, ke, acc);
     else if (s == 1) x_tiles<K, 1>(Mg, p, x, hi, kb, ke, acc);
     else x_tiles<K, 2>(Mg, p, x, hi, kb, ke, acc);
   }
@@ -1361,7 +1422,7 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   int rc;
   if ((rc = lds_opt_in(c, sums ? 3 : 2, sums ? &fin_kernel<K, true> : &fin_kernel<K, false>, FT<K>::LDS)))
     return rc;
-  const int lds = (FT<K>::MS + (FT<K>::PLDS ? c->R * T::K3 : 0)) * 8;  // p staged for R ratings
+  const int lds = (FT<K>::MS + (FT<K>::PLDS ? c->R * T::K3 : 0) + (FT<K>::PLB ? FT<K>::PLN : 0)) * 8;
   SpRange spr{};
   for (int r = 0; r < c->R; ++r) {
     spr.lo[r] = h.sp_lo[r];

@@ -444,7 +444,9 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     }
     st_.mark(2);
   }
-  if constexpr (MODE != SK_LL) __syncthreads();  // every wave's share of P^s staged
+  // pass B staged P^s without a barrier (it forms no V tables): publish it before X; the other
+  // modes published it before the V tables, so their waves run X and S without waiting
+  if constexpr (MODE == SK_B) __syncthreads();
   if (un.nst > 0) {
     const int nst = un.nst;
     if constexpr (MODE != SK_LL) {
