@@ -35,6 +35,9 @@ enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
 #ifndef MMSBM_SK_TRSWZ
 #define MMSBM_SK_TRSWZ 1  // the Z operand transpose with a bank swizzle (r03u A/B: 38.5k vs 38.1k iter/s)
 #endif
+#ifndef MMSBM_SK_SCOOP
+#define MMSBM_SK_SCOOP 1  // the workgroup's S partial in one cooperative pass (0: per-wave shares + tree)
+#endif
 #ifndef MMSBM_SK_MRED
 #define MMSBM_SK_MRED 0  // 1: d's sum over b on MFMA, four chunks at a time (measured slower than the DPP row sum)
 #endif
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
           if (4 * tt + hi < nst && blk < NG && z < K) xb[(size_t)un.prow[tt] * K + z] = xacc;
         }
       }
-      if (MODE == SK_A || (MODE == SK_U && s == 0)) {
+      if (!MMSBM_SK_SCOOP && (MODE == SK_A || (MODE == SK_U && s == 0))) {
         // ---- S_r[a][cell] += sum_q theta_{g_q}[a] M_q[cell] (m = a, k = q, n = cell), the
         // unit's row tiles in order
 #pragma unroll
@@ -489,6 +492,51 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     }
   }
 
+#if MMSBM_SK_SCOOP
+  if (MODE == SK_A || (MODE == SK_U && s == 0)) {  // (workgroup-uniform)
+    // ---- the workgroup's S partial in one pass over all its stretches: S_r[a][cell] =
+    // sum_q theta_{g_q}[a] M_q[cell] over the rows q = (wave, slot) of every wave, in that order
+    // (m = a, k = q, n = cell; A from the waves' pivot theta rows, B from their M rows).  Rows of
+    // absent stretches are zero (V zeros, zero theta); an empty slot zeroes its own first.  One
+    // barrier, then each wave takes (a tile, cell group) items and stores its cells directly.
+    constexpr int WV = MODE == SK_U ? T::WAVE_U : T::WAVE;
+    if (un.nst == 0) {
+#pragma unroll
+      for (int i = 0; i < (GUK * SLOT + 63) / 64; ++i)
+        if (lane + 64 * i < GUK * SLOT) MSl[lane + 64 * i] = 0.0;
+#pragma unroll
+      for (int i = 0; i < (T::THL + 63) / 64; ++i)
+        if (lane + 64 * i < T::THL) THl[lane + 64 * i] = 0.0;
+    }
+    __syncthreads();
+    double* __restrict__ out = spart + ((size_t)b * n_wg + w) * K3;
+    constexpr int NI = NG * NCG, NIW = (NI + NW - 1) / NW, QS = NW * GUK / 4;
+    double acc[NIW];
+#pragma unroll
+    for (int j = 0; j < NIW; ++j) acc[j] = 0.0;
+#pragma unroll 4
+    for (int qs = 0; qs < QS; ++qs) {
+      const int qw = (4 * qs) / GUK, qt = (4 * qs) % GUK + hi;  // (wave qw uniform per step)
+      const double* __restrict__ wq = smem + T::PSD + qw * WV;
+      const double* __restrict__ thq = wq + GUK * SLOT + SK_ROWS + qt * 4 * NG + lo;
+      const double* __restrict__ mq = wq + qt * SLOT + 4 * blk + lo;
+#pragma unroll
+      for (int j = 0; j < NIW; ++j) {
+        const int it = wv + NW * j;
+        if (j + 1 < NIW || it < NI) {  // (uniform)
+          const int at = it / NCG, cg = it % NCG;
+          acc[j] = mfma4(thq[4 * at], mq[16 * cg], acc[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NIW; ++j) {
+      const int it = wv + NW * j;
+      const int a = 4 * (it / NCG) + hi, cell = 16 * (it % NCG) + 4 * blk + lo;
+      if (it < NI && a < K && cell < K2) out[a * K2 + cell] = acc[j];
+    }
+  }
+#else
   if (MODE == SK_A || (MODE == SK_U && s == 0)) {  // (workgroup-uniform)
     // ---- the workgroup's S partial: the 8 waves' shares added in a fixed order,
     // ((w0 + w4) + (w2 + w6)) + ((w1 + w5) + (w3 + w7)), through LDS: waves 4-7 park theirs, waves
@@ -525,6 +573,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
       }
     }
   }
+#endif
   if constexpr (MODE == SK_LL) {
     __shared__ double redl[NW];
     ll = wave_sum(ll);
