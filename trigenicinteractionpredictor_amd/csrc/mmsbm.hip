@@ -1750,9 +1750,11 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
       units_b = b;
     }
   }
+  int rho = 85;  // stream-0 unit length, % of the others' (fused plans; plan.h)
+  if (const char* e = getenv("MMSBM_SK_RHO")) rho = std::max(10, std::min(100, atoi(e)));
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
                            c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, 1024, c->sk_fused,
-                           mmsbm_plan::sk_gu(c->K));
+                           mmsbm_plan::sk_gu(c->K), rho);
   const auto& h = sd.h;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;

@@ -19,6 +19,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <vector>
 
@@ -198,7 +199,7 @@ inline void make_slots(Plan& pl) {
 // K^3 partial, so large K wants more rows per partial).
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
-                  int wg_target = 1024, bool fill = false, int gu = GU) {
+                  int wg_target = 1024, bool fill = false, int gu = GU, int rho_pct = 85) {
   Plan pl;
   pl.gu = std::max(1, std::min(gu, GU));
   pl.R = R;
@@ -247,14 +248,18 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   // unit length: the work spread over about units_* units, but no unit longer than LCAP chunks
   // (large link sets get more units rather than longer ones, so a few long units do not set
   // the kernel's duration).  Fill-packed small plans (the fused launch) take units_a as the
-  // number of units for all streams together (about the waves that are resident at once) and
-  // one length for every stream, at least one block.
+  // number of units for all streams together (about the waves that are resident at once); a
+  // stream-0 unit is rho_pct % of the others' length (it also owns its genes' X contraction and
+  // S outer products, so a shorter chunk loop evens the waves' finish; 85 % measured best of
+  // 55 / 70 / 85 / 100 on fold0 K=10, profiles/r03ad_rho_ab.txt), streams 1 / 2 at least one block.
   const long long LCAP = small ? LCAP_SK : 64;
   int lmax_a = (int)std::min(LCAP, std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1)));
   int lmax_b = (int)std::min(LCAP, std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1)));
   if (small && fill) {
-    const long long all = chunks_a + chunks_b;
-    lmax_a = lmax_b = (int)std::min(LCAP, std::max<long long>(SK_BLOCK, (all + units_a - 1) / std::max(units_a, 1)));
+    const double rho = std::max(10, std::min(100, rho_pct)) / 100.0;
+    const double lb = ((double)chunks_a / rho + (double)chunks_b) / std::max(units_a, 1);
+    lmax_b = (int)std::min<double>(LCAP, std::max<double>(SK_BLOCK, std::ceil(lb)));
+    lmax_a = (int)std::min<double>(LCAP, std::max<double>(rho < 1.0 ? 4.0 : SK_BLOCK, std::ceil(rho * lb)));
   }
   pl.lmax[0] = lmax_a;
   pl.lmax[1] = lmax_b;
