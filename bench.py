@@ -69,6 +69,14 @@ def parse():
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and run the end-of-run gather without any GPU work "
                          "(CPU test of the N-rank launch path, with --backend gloo)")
+    ap.add_argument("--process-group", action="store_true",
+                    help="create the process group at --gpus 1 too (world size 1): the nccl init "
+                         "with device_id, the RCCL all-gather of the result rows, the replay check "
+                         "and, with --shard links, the per-iteration RCCL all-reduce all run on the "
+                         "one GPU (VERDICT r3 item 4)")
+    ap.add_argument("--test-frac", type=float, default=0.2,
+                    help="share of the E unique triples that go to the test file (config 5 runs "
+                         "with 0: all E links train)")
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="processes for the aggregate CPU baseline (default: the host cores this "
                          "process may use, at most 16)")
@@ -201,8 +209,17 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
     traffic = None
     if pmc is not None:
         traffic = sum(pmc[1]["hbm_bytes_per_launch"].get(k, 0.0) for k in work)
-    return {"bound": "mfma", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": tf / FP64_PEAK_TFLOPS,
+    exe_tf = exe / iter_s / 1e12
+    # the 8d credit counts the reference's 8 K^3 per observation; where that exceeds the FP64
+    # peak (K >= 20 here: the factorisation does far less work) it says nothing about utilisation,
+    # so the headline becomes the executed FLOPs and the credit stays beside it
+    credited = tf <= FP64_PEAK_TFLOPS
+    head = tf if credited else exe_tf
+    return {"bound": "mfma", "achieved": head, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": head / FP64_PEAK_TFLOPS,
+            "frac_basis": ("SURVEY 8d credited FLOPs" if credited else
+                           "executed FLOPs (the 8d credit exceeds the FP64 peak)"),
+            "credited": {"achieved": tf, "frac": tf / FP64_PEAK_TFLOPS},
             "traffic": traffic,
             "traffic_unit": "HBM bytes per iteration (PMC FETCH_SIZE x 2 + WRITE_SIZE, all kernels)",
             "traffic_source": None if pmc is None else pmc[0],
@@ -224,12 +241,12 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
                                 pmc[1]["hbm_bytes_per_launch"].get(dom)}}
 
 
-def make_fold(P, E, rank, hub=""):
+def make_fold(P, E, rank, hub="", test_frac=0.2):
     from trigenicinteractionpredictor_amd.data import FoldSpec, write_fold
     d = tempfile.mkdtemp(prefix="mmsbm_bench_r%d_" % rank)
     tr, te = os.path.join(d, "train0.dat"), os.path.join(d, "test0.dat")
     hf, hs = (float(x) for x in hub.split(",")) if hub else (0.0, 0.0)
-    write_fold(FoldSpec(P=P, E=E, seed=7, hub_frac=hf, hub_share=hs), tr, te)
+    write_fold(FoldSpec(P=P, E=E, seed=7, hub_frac=hf, hub_share=hs, test_frac=test_frac), tr, te)
     return tr, te
 
 
@@ -345,7 +362,7 @@ def main():
     if args.launch_check:
         launch_check(args, world, rank)
         return 0
-    train, test = make_fold(args.P, args.E, rank, args.hub)
+    train, test = make_fold(args.P, args.E, rank, args.hub, args.test_frac)
     cpu_rec = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = args.cpu_cores or min(len(os.sched_getaffinity(0)), 16)
@@ -357,8 +374,17 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     coll = dev if args.backend == "nccl" else torch.device("cpu")  # where collectives run
-    if world > 1:
+    dist_on = world > 1 or args.process_group
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            import socket
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            if "MASTER_PORT" not in os.environ:
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -409,22 +435,23 @@ def main():
     torch.cuda.synchronize(dev)
     in_loop = {k: eng.timing_result(k) for k in eng.KERNELS}
     eng.timing(False)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     runner.iterate(args.steps)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     # each kernel of the iteration alone, back to back on the launch stream (per-launch duration
     # for the roofline; the in-loop events above also time the dependent-launch boundary)
-    b2b = {k: eng.time_kernel(k, args.roofline_launches) for k in eng.KERNELS}
+    launched = eng.launched_kernels()
+    b2b = {k: eng.time_kernel(k, args.roofline_launches) for k in launched}
     elapsed = t1 - t0
     L = runner.loglik(0)
     rows = result_rows(sample_ids, L)
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -432,7 +459,7 @@ def main():
             rows = gather_rows(rows, B * world, device=coll)
     n_gathered = int(rows.shape[0])
     scale_check = None
-    if rank == 0 and world > 1 and not links_mode:
+    if rank == 0 and dist_on and not links_mode:
         # every sample replayed as ONE batch on this GPU: a sample's bits do not depend on its
         # batch or rank, so the gathered values must equal the replay bit for bit
         def factory(nb):
@@ -470,7 +497,8 @@ def main():
                        "P": host.P, "E_train": int(ids.shape[0]), "E_test": int(tids.shape[0]),
                        "E_obs": E_obs, "samples_per_gpu": B,
                        "parallelism": ("link-sharded x%d" if links_mode else "restart-sharded x%d") % world},
-            "world_size": dist.get_world_size() if world > 1 else 1,
+            "world_size": dist.get_world_size() if dist_on else 1,
+            "process_group": dist.get_backend() if dist_on else None,
             "gathered_samples": n_gathered,
             "final_loglik": float(rows[0, 1]),
             "final_loglik_best": float(rows[:, 1].max()),
@@ -480,8 +508,11 @@ def main():
             "build_id": build_id,
             "roofline": roofline,
             "iteration": {"us": iter_s * 1e6},
-            "kernel_us": {k: {"back_to_back": b2b[k] * 1e3,
-                              "in_loop": in_loop[k][0] * 1e3 / max(in_loop[k][1], 1)}
+            # kernels the iteration does not launch (the fused small-K E-step has no pass B) are
+            # null: their event pairs would only time the events themselves
+            "kernel_us": {k: ({"back_to_back": b2b[k] * 1e3,
+                               "in_loop": in_loop[k][0] * 1e3 / max(in_loop[k][1], 1)}
+                              if k in launched else None)
                           for k in eng.KERNELS},
             "plan": plan,
             "cpu_baseline": cpu_rec,
@@ -493,7 +524,7 @@ def main():
     if scale_check is not None and not scale_check["bitwise_equal"]:
         print("bench.py: gathered per-sample results differ from the one-GPU replay", file=sys.stderr)
         rc = 3
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     return rc

@@ -139,3 +139,90 @@ def test_batch_mode_matches_reference_loop(tmp_path):
     got = [l for l in lines if l.startswith("Sample ") and "iterations" in l]
     assert [(int(l.split()[1][:-1]), int(l.split()[2])) for l in got] == [(s, it) for s, it, _ in ref]
     assert [w[0] for w in written] == [out + "Sample_%d_K2.csv" % s for s, _, c in ref if c]
+
+
+class _FileModel:
+    """Model stand-in whose to_file writes the converged snapshot exactly (repr of every value),
+    so two runs' files are equal byte for byte only when their results are."""
+
+    @staticmethod
+    def make():
+        from trigenicinteractionpredictor_amd.model import Model
+
+        class M(Model):
+            def to_file(self, name_file=None):
+                with open(name_file, "w") as f:
+                    f.write("L %r\n" % self.likelihood)
+                    f.write("theta %r\n" % [list(map(float, r)) for r in self._theta])
+                    f.write("pr %r\n" % repr(self._pr))
+        return M()
+
+
+def _ranked_worker(rank, world, port, argv, queue):
+    import torch.distributed as dist  # noqa: F401
+    from oracle_engine import OracleEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    holder = {}
+
+    def factory():
+        holder["m"] = _FileModel.make()
+        return holder["m"]
+
+    lines = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        rc = cli.main(argv + ["--gpus", str(world), "--backend", "gloo"], model_factory=factory,
+                      out=lines.append,
+                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links))
+    queue.put((rank, rc, lines))
+
+
+def test_two_rank_gloo_cli_writes_the_one_rank_files(tmp_path):
+    """`--gpus 2` (two ranks, gloo, the C oracle as each rank's engine): the Sample_<n>_K<k>.csv
+    files are byte-identical to a one-process `--batch` run's, and rank 0 prints every sample's
+    summary line in sample order (src/run.sh:36-45, :1253-1279)."""
+    import multiprocessing as mp
+
+    from oracle_engine import OracleEngine
+    one, two = tmp_path / "one", tmp_path / "two"
+    one.mkdir()
+    two.mkdir()
+    base = ["-k", "2", "-i", "40", "-n", "5", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST, "--seed", "5",
+            "--batch", "2"]
+    holder = {}
+
+    def factory():
+        holder["m"] = _FileModel.make()
+        return holder["m"]
+
+    lines1 = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        rc = cli.main(base + ["-o", str(one) + os.sep], model_factory=factory, out=lines1.append,
+                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links))
+    assert rc == 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 250) % 1000
+    argv = base + ["-o", str(two) + os.sep]
+    procs = [ctx.Process(target=_ranked_worker, args=(r, 2, port, argv, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {r: (rc, lines) for r, rc, lines in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert got[0][0] == 0 and got[1][0] == 0
+    assert got[1][1] == []                                   # rank 1 prints nothing
+    files1, files2 = sorted(os.listdir(one)), sorted(os.listdir(two))
+    assert files1 and files1 == files2
+    for f in files1:
+        assert (one / f).read_bytes() == (two / f).read_bytes()
+    summary = lambda ls: [l for l in ls if l.startswith("Sample ") and "iterations" in l]  # noqa: E731
+    assert summary(got[0][1]) == summary(lines1)
+
+
+def test_gpus_flag_validation():
+    rc, _ = _run(["--gpus", "0"])
+    assert rc == 2
+    rc, _ = _run(["--gpus", "2", "--backend", "mpi"])
+    assert rc == 2

@@ -76,24 +76,70 @@ def test_config1_fold0_K2_50_iterations(tmp_path):
     np.testing.assert_allclose(eng.loglik(1)[0], c_oracle.loglik(tids, tcounts, th_o, pr_o), rtol=RTOL)
 
 
+def _oracle_snapshots(ids, counts, th, pr, at):
+    """The C oracle's (theta, p) after each iteration count in `at` (ascending)."""
+    from oracle import c_oracle
+    out, done = [], 0
+    for n in at:
+        for _ in range(n - done):
+            th, pr = c_oracle.make_iteration(ids, counts, th, pr)
+        done = n
+        out.append((th, pr))
+    return out
+
+
+def _parallel(fn, items):
+    """fn over items on host threads (the C oracle releases the GIL inside its ctypes calls)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(8, len(items))) as ex:
+        return list(ex.map(fn, items))
+
+
+def test_config2_fold0_K10_at_1_5_25_iterations(tmp_path):
+    """Config 2 (the headline): fold0 stand-in, K=10, 1 sample, against the C oracle after 1, 5
+    and 25 iterations: theta, p and the train / held-out likelihoods."""
+    from oracle import c_oracle
+    from trigenicinteractionpredictor_amd.data import FOLD0
+    m = _model(tmp_path, FOLD0)
+    th, pr = _samples(m, 10, 1, 11)
+    eng = _engine(m, 10, 1, th, pr)
+    ids, counts = m._link_arrays(0)
+    tids, tcounts = m._link_arrays(1)
+    want = _oracle_snapshots(ids, counts, th[0], pr[0], (1, 5, 25))
+    done = 0
+    for n, (th_o, pr_o) in zip((1, 5, 25), want):
+        eng.iterate(n - done)
+        done = n
+        t, p = eng.download()
+        np.testing.assert_allclose(t[0], th_o, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(p[0], pr_o, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(eng.loglik(0)[0], c_oracle.loglik(ids, counts, th_o, pr_o), rtol=RTOL)
+        np.testing.assert_allclose(eng.loglik(1)[0], c_oracle.loglik(tids, tcounts, th_o, pr_o), rtol=RTOL)
+
+
 def test_config3_fold0_K20_batch8(tmp_path):
-    """Config 3's per-GPU share: fold0 stand-in, K=20, 8 samples in one batched engine, 2
-    iterations; samples 0 and 7 (first and last of the batch) against the oracle."""
+    """Config 3's per-GPU share: fold0 stand-in, K=20, 8 samples in one batched engine; EVERY
+    sample against the C oracle after 2 and after 5 iterations (theta, p, train L)."""
     from oracle import c_oracle
     from trigenicinteractionpredictor_amd.data import FOLD0
     m = _model(tmp_path, FOLD0)
     th, pr = _samples(m, 20, 8, 3)
     eng = _engine(m, 20, 8, th, pr)
-    eng.iterate(2)
-    t, p = eng.download()
-    L = eng.loglik(0)
     ids, counts = m._link_arrays(0)
-    for s in (0, 7):
-        th_o, pr_o = _oracle(ids, counts, th[s], pr[s], 2)
-        np.testing.assert_allclose(t[s], th_o, rtol=RTOL, atol=ATOL)
-        np.testing.assert_allclose(p[s], pr_o, rtol=RTOL, atol=ATOL)
-        np.testing.assert_allclose(L[s], c_oracle.loglik(ids, counts, th_o, pr_o), rtol=RTOL)
-    assert np.isfinite(t).all() and np.isfinite(p).all()
+    want = _parallel(lambda s: _oracle_snapshots(ids, counts, th[s], pr[s], (2, 5)), list(range(8)))
+    done = 0
+    for k, n in enumerate((2, 5)):
+        eng.iterate(n - done)
+        done = n
+        t, p = eng.download()
+        L = eng.loglik(0)
+        assert np.isfinite(t).all() and np.isfinite(p).all()
+        Lo = _parallel(lambda s: c_oracle.loglik(ids, counts, *want[s][k]), list(range(8)))
+        for s in range(8):
+            th_o, pr_o = want[s][k]
+            np.testing.assert_allclose(t[s], th_o, rtol=RTOL, atol=ATOL)
+            np.testing.assert_allclose(p[s], pr_o, rtol=RTOL, atol=ATOL)
+            np.testing.assert_allclose(L[s], Lo[s], rtol=RTOL)
 
 
 def test_config4_all_train_multicount_K10_batch8(tmp_path):
@@ -232,6 +278,32 @@ def test_config5_block_against_oracle(c5):
     np.testing.assert_allclose(n[0].cpu().numpy(), n_o, rtol=RTOL, atol=1e-300)
     np.testing.assert_allclose(s[0].cpu().numpy(), s_o, rtol=RTOL, atol=1e-300)
     e.close()
+
+
+def test_config5_subfold_full_iteration_against_oracle(c5):
+    """A 60,000-link sub-fold of the 10M set (links 3,000,000-3,060,000) as a fold of its own:
+    its genes renumbered densely (ascending ids), its own degree, one full EM iteration at
+    K=30 (theta, p, train L before and after) against the C oracle."""
+    from oracle import c_oracle
+    from trigenicinteractionpredictor_amd import EMEngine
+    P, ids, counts, th, pr = c5
+    sub = ids[3_000_000:3_060_000]
+    genes, inv = np.unique(sub.ravel(), return_inverse=True)
+    sids = np.ascontiguousarray(inv.reshape(-1, 3).astype(np.int32))
+    scounts = np.ascontiguousarray(counts[3_000_000:3_060_000])
+    sth = np.ascontiguousarray(th[genes])
+    eng = EMEngine(C5_K, genes.size, B=1)
+    eng.set_links(0, sids, scounts)
+    eng.upload(sth[None], pr[None])
+    L0 = eng.loglik(0)[0]
+    eng.iterate(1)
+    t, p = eng.download()
+    th_o, pr_o = c_oracle.make_iteration(sids, scounts, sth, pr)
+    np.testing.assert_allclose(L0, c_oracle.loglik(sids, scounts, sth, pr), rtol=RTOL)
+    np.testing.assert_allclose(t[0], th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(p[0], pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(eng.loglik(0)[0], c_oracle.loglik(sids, scounts, th_o, pr_o), rtol=RTOL)
+    eng.close()
 
 
 def test_restart_driver_on_gpu_matches_oracle_driver(tmp_path):

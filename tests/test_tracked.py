@@ -81,3 +81,61 @@ def test_model_link_arrays_follow_in_place_edits():
     assert tids.tolist() == [[0, 1, 2]] and tcounts.tolist() == [[0, 1]]
     m.links = dict(m.links)                                            # assigned plain dict
     assert isinstance(m.links, TrackedLinks)
+
+
+def test_assigned_dict_stays_aliased():
+    """`m.links = d` keeps `d` as the table's source: row edits of `d` are seen at
+    once, edits through `m.links` reach `d`, and keys added to `d` itself arrive with
+    links_changed()."""
+    m = Model()
+    m.P = 6
+    d = {"0_1_2": [1, 0], "1_2_3": [0, 1]}
+    m.links = d
+    v0 = version_of(m._links)
+    ids0, counts0 = m._link_arrays(0)
+    d["0_1_2"][1] += 2                                   # the caller's own dict
+    assert version_of(m._links) != v0
+    assert m._link_arrays(0)[1].tolist() == [[1, 2], [0, 1]]
+    m.links["3_4_5"] = [1, 1]                            # through the model
+    assert d["3_4_5"] == [1, 1]
+    del m.links["1_2_3"]
+    assert "1_2_3" not in d
+    d["2_3_4"] = [0, 3]                                  # a new key in the source: declared
+    v1 = version_of(m._links)
+    m.links_changed()
+    assert version_of(m._links) != v1
+    ids, counts = m._link_arrays(0)
+    assert ids.tolist() == [[0, 1, 2], [3, 4, 5], [2, 3, 4]]
+    assert counts.tolist() == [[1, 2], [1, 1], [0, 3]]
+    assert m.links == d
+
+
+def test_model_deepcopy_and_pickle_keep_tracked_tables():
+    """copy.deepcopy / pickle of a Model: the copy's tables are tracked (the next
+    engine call can read their versions) and equal the original's."""
+    g = os.path.join(GOLDEN, "tiny")
+    m = Model()
+    m.get_traintest(os.path.join(g, "train.dat"), os.path.join(g, "test.dat"))
+    _ = m.links                                           # one table materialised, one lazy
+    for clone in (copy.deepcopy(m), pickle.loads(pickle.dumps(m))):
+        assert isinstance(clone._links, TrackedLinks) and clone._engine is None
+        assert version_of(clone._links) and clone.links == m.links
+        assert clone.test_links == m.test_links
+        np.testing.assert_array_equal(clone._link_arrays(0)[1], m._link_arrays(0)[1])
+        clone.links[next(iter(clone.links))][0] += 1     # edits stay seen in the copy
+        assert clone._link_arrays(0)[1][0, 0] == m._link_arrays(0)[1][0, 0] + 1
+
+
+def test_joint_model_deepcopy_and_alias():
+    from trigenicinteractionpredictor_amd import joint
+    mj = joint.Model()
+    d = {"0_1_2": [1, 0]}
+    mj.links = d
+    d["0_1_2"][0] += 1
+    assert mj.links["0_1_2"] == [2, 0]
+    d["1_2_3"] = [0, 1]
+    mj.links_changed()
+    assert "1_2_3" in mj.links
+    clone = copy.deepcopy(mj)
+    assert isinstance(clone.links, TrackedLinks) and clone.links == mj.links
+    assert version_of(clone.links) and version_of(clone.dlinks)

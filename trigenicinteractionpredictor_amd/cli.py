@@ -15,6 +15,17 @@ Same flags, defaults, validation, exit codes and per-sample semantics as the ref
   * the K = 1 warning never prints (`int(arg == 1)`, :1224) — kept.
 The iterations between two checks run as one `Model.make_iterations(n)` call (no host round
 trip per iteration); the per-iteration lines are printed after the batch, with the same text.
+
+`--gpus N` is the reference's process-level sample parallelism (src/run.sh:36-45, one OS process
+per batch of samples) as one process per GPU: without a launcher the command starts N copies of
+itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them) before it
+touches a GPU, and every rank takes a contiguous block of the pending samples (`run_ranked`).
+Each rank replays the one RNG stream through the draws of the samples before its block, so a
+sample starts from the state the one-process run gives it, runs with the reference's check
+schedule and convergence rule (:1262-1279) on its own GPU, and writes its own
+`Sample_<n>_K<k>.csv`.  One all-gather at the end (RCCL over xGMI under nccl) brings every
+sample's result to rank 0, which prints the summary.  A sample's bits depend neither on its batch
+nor on its rank, so the files equal a one-process run's byte for byte.
 """
 from __future__ import annotations
 
@@ -32,6 +43,8 @@ python -m trigenicinteractionpredictor_amd.cli [-h|--help] [-i|--num_iterations=
     [-o|--out=] <output path prefix> [-t|--train=] <train file> [-e|--test=] <test file>
     [-k|--k=] <number of groups> [--seed=] <RNG seed, default: the process id>
     [--batch=] <samples advanced together on the GPU, default 1>
+    [--gpus=] <processes, one per GPU, over which the samples are sharded, default 1>
+    [--backend=] <collective backend of --gpus: nccl (RCCL, default) or gloo>
 
 Defaults: iterations {it}, samples {s}, check frequency {f}, train file {t}, K {k}.
 """
@@ -49,7 +62,8 @@ def parse(argv, defaults):
     try:
         opts, _ = getopt.getopt(argv, "hi:n:s:f:b:o:t:e:k:",
                                 ["help", "num_iterations=", "num_samples=", "sample_ini=", "fcheck=",
-                                 "bcheck=", "out=", "train=", "test=", "k=", "seed=", "batch="])
+                                 "bcheck=", "out=", "train=", "test=", "k=", "seed=", "batch=", "gpus=",
+                                 "backend="])
     except getopt.GetoptError:
         print("Argument error. Aborting")
         raise ArgError()
@@ -117,6 +131,16 @@ def parse(argv, defaults):
                     print("\n\nERROR: batch size should be a positive integer number")
                     raise ArgError()
                 cfg["batch"] = int(arg)
+            elif opt == "--gpus":
+                if int(arg) < 1:
+                    print("\n\nERROR: number of GPUs should be a positive integer number")
+                    raise ArgError()
+                cfg["gpus"] = int(arg)
+            elif opt == "--backend":
+                if arg not in ("nccl", "gloo"):
+                    print("\n\nERROR: backend should be nccl or gloo")
+                    raise ArgError()
+                cfg["backend"] = arg
         except ValueError:
             raise ArgError()
     return cfg
@@ -158,7 +182,32 @@ def run_sample(model, cfg, sample, outfile, out=print):
 
 
 DEFAULTS = {"iterations": 10000, "samples": 100, "sample_ini": 0, "fcheck": 25, "bcheck": 100,
-            "train": "train0.dat", "test": "test0.dat", "out": "", "k": 1, "seed": None, "batch": 1}
+            "train": "train0.dat", "test": "test0.dat", "out": "", "k": 1, "seed": None, "batch": 1,
+            "gpus": 1, "backend": "nccl"}
+
+
+def _write_result(model, cfg, r):
+    """A converged sample's file (:1275) from its theta / p snapshot and converged likelihood."""
+    model.theta = r.theta.tolist()
+    model.pr = r.pr.tolist()
+    model.likelihood = r.loglik
+    model.to_file(cfg["out"] + "Sample_" + str(r.sample) + "_K" + str(cfg["k"]) + ".csv")
+
+
+def _summary(r):
+    return ("Sample " + str(r.sample) + ": " + str(r.iterations) + " iterations, likelihood "
+            + str(r.loglik) + (" (converged)" if r.converged else ""))
+
+
+def _default_engine_factory(model, K):
+    from .engine import EMEngine
+
+    def factory(n):
+        eng = EMEngine(K, model.P, B=n, R=model.R, eps=model.eps)
+        eng.set_links(0, *model._link_arrays(0))
+        eng.set_links(1, *model._link_arrays(1))
+        return eng
+    return factory
 
 
 def run_batch(model, cfg, samples, out=print, engine_factory=None):
@@ -172,13 +221,7 @@ def run_batch(model, cfg, samples, out=print, engine_factory=None):
     from .restarts import run_samples
     K, B = cfg["k"], cfg["batch"]
     if engine_factory is None:
-        from .engine import EMEngine
-
-        def engine_factory(n):
-            eng = EMEngine(K, model.P, B=n, R=model.R, eps=model.eps)
-            eng.set_links(0, *model._link_arrays(0))
-            eng.set_links(1, *model._link_arrays(1))
-            return eng
+        engine_factory = _default_engine_factory(model, K)
     done = []
     for lo in range(0, len(samples), B):
         block = samples[lo:lo + B]
@@ -190,26 +233,126 @@ def run_batch(model, cfg, samples, out=print, engine_factory=None):
         res = run_samples(engine_factory(len(block)), block, thetas, prs, cfg["iterations"],
                           cfg["fcheck"], cfg["bcheck"], keep_params=True)
         for r in res:
-            out("Sample " + str(r.sample) + ": " + str(r.iterations) + " iterations, likelihood "
-                + str(r.loglik) + (" (converged)" if r.converged else ""))
+            out(_summary(r))
             if r.converged:
-                model.theta = r.theta.tolist()
-                model.pr = r.pr.tolist()
-                model.likelihood = r.loglik
-                model.to_file(cfg["out"] + "Sample_" + str(r.sample) + "_K" + str(K) + ".csv")
+                _write_result(model, cfg, r)
             done.append((r.sample, r.iterations, r.converged))
     return done
 
 
+def run_ranked(model, cfg, samples, out=print, engine_factory=None, group=None, device=None):
+    """`--gpus N`, one rank: this rank's contiguous block of the pending `samples` (the same list
+    on every rank), advanced `--batch` at a time with the reference's per-sample check schedule
+    and convergence rule (restarts.run_samples), converged samples written by this rank; then
+    one all-gather (restarts.gather_results: RCCL over xGMI under nccl) of every rank's
+    (sample, iterations, converged, likelihood, held-out likelihood).  Rank 0 prints one summary
+    line per sample, in sample order, as run_batch does.  Returns the gathered results."""
+    import numpy as np
+    import torch.distributed as dist
+    from .restarts import gather_results, run_samples, shard_samples
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    K, B = cfg["k"], cfg["batch"]
+    mine = set(shard_samples(len(samples), world, rank))
+    states = {}
+    for i, s in enumerate(samples):          # the one stream, in sample order (:1260)
+        model.initialize_parameters(K)
+        if i in mine:
+            states[s] = (np.array(model._theta, dtype=np.float64), np.array(model._pr, dtype=np.float64))
+    block = [s for i, s in enumerate(samples) if i in mine]
+    if block and engine_factory is None:
+        engine_factory = _default_engine_factory(model, K)
+    local = []
+    for lo in range(0, len(block), B):
+        part = block[lo:lo + B]
+        res = run_samples(engine_factory(len(part)), part, [states[s][0] for s in part],
+                          [states[s][1] for s in part], cfg["iterations"], cfg["fcheck"], cfg["bcheck"],
+                          keep_params=True)
+        for r in res:
+            if r.converged:
+                _write_result(model, cfg, r)
+        local += res
+    rows = gather_results(local, len(samples), group=group, device=device)
+    if rank == 0:
+        for r in rows:
+            out(_summary(r))
+    return rows
+
+
+def spawn_ranks(n, argv):
+    """`--gpus N` without a launcher: N copies of this command, one rank per GPU, started before
+    this process touches a GPU; returns the worst exit code.  The parent's seed is passed on, so
+    every rank replays the same RNG stream (:1149 seeds it once per run)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    if not any(a == "--seed" or a.startswith("--seed=") for a in argv):
+        argv = list(argv) + ["--seed", str(os.getpid())]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-m", "trigenicinteractionpredictor_amd.cli", *argv],
+                                      env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        if code != 0:
+            rc = rc or (code if code > 0 else 128 - code)
+            for q in procs:
+                if q.poll() is None:
+                    q.terminate()
+    return rc
+
+
 def main(argv=None, model_factory=None, out=print, engine_factory=None):
+    argv = sys.argv[1:] if argv is None else argv
     cfg = dict(DEFAULTS)
     cfg["seed"] = os.getpid()                                    # :1149
     try:
-        cfg = parse(sys.argv[1:] if argv is None else argv, cfg)
+        cfg = parse(argv, cfg)
     except ArgError:
         return 2
     if cfg.get("help"):
         return 0
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if cfg["gpus"] > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(cfg["gpus"], argv)                   # before any GPU call
+    if world != cfg["gpus"]:
+        out("\n\nERROR: WORLD_SIZE=%d but --gpus %d" % (world, cfg["gpus"]))
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    group_on = world > 1
+    device = None
+    if group_on:
+        import torch
+        import torch.distributed as dist
+        if cfg["backend"] == "nccl":
+            local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(local)
+            device = torch.device("cuda", local)
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            if torch.cuda.is_available():           # ranks sharing the box's GPUs (rehearsal)
+                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+            dist.init_process_group("gloo")
+        if rank != 0:
+            out = _quiet
+    try:
+        return _main_ranked(cfg, model_factory, out, engine_factory, group_on, device)
+    finally:
+        if group_on:
+            import torch.distributed as dist
+            dist.barrier()
+            dist.destroy_process_group()
+
+
+def _quiet(*_a, **_k):
+    return None
+
+
+def _main_ranked(cfg, model_factory, out, engine_factory, group_on, device):
     random.seed(cfg["seed"])
     if int(cfg["fcheck"]) > int(cfg["iterations"]):
         out("\n\nWARNING: the likelihood frequency checking is bigger that the number of num_iterations "
@@ -232,11 +375,15 @@ def main(argv=None, model_factory=None, out=print, engine_factory=None):
         outfile = cfg["out"] + "Sample_" + str(sample) + "_K" + str(cfg["k"]) + ".csv"
         if os.path.isfile(outfile):                              # :1256-1257
             continue
-        if cfg["batch"] > 1:
+        if cfg["batch"] > 1 or group_on:
             pending.append(sample)
         else:
             run_sample(model, cfg, sample, outfile, out)
-    if pending:
+    if group_on:
+        import torch.distributed as dist
+        dist.barrier()           # every rank has its pending list before any rank writes a file
+        run_ranked(model, cfg, pending, out, engine_factory, device=device)
+    elif pending:
         run_batch(model, cfg, pending, out, engine_factory)
     return 0
 

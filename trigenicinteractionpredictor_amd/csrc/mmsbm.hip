@@ -1236,6 +1236,8 @@ struct SetDev {  // device copy of one link set's plan
   int* sku[2] = {nullptr, nullptr};     // small-K plans (sk.h): slot descriptors of each group,
   int4* skr[2] = {nullptr, nullptr};    // slot-major records,
   int* skrow12 = nullptr;               // slot-major row12 of group 0
+  int ncu = 0;                          // CUs the fused plan's unit target came from (0: none)
+  int unit_target = 0;
   void release() {
     void* ps[] = {rows, chunk_prow, chunk_vslot, wg_units, wg_code, wg_gene, vgenes, prow_ptr, prow_gene, sp_desc,
                   sku[0], sku[1], skr[0], skr[1], skrow12};
@@ -1700,7 +1702,14 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
     }
     c->sk = sk;
     const char* f = getenv("MMSBM_SK_FUSED");  // the fused E-step (SK_U); 0: pass A + pass B
-    c->sk_fused = sk && !(f && f[0] == '0');
+    const bool fused = sk && !(f && f[0] == '0');
+    if (fused != c->sk_fused) {  // the fused plan packs its units differently: set links again
+      DeviceGuard g(c->device);
+      for (auto& sd : c->sets) sd.release();
+      c->ws = nullptr;
+      c->ws_bytes = 0;
+    }
+    c->sk_fused = fused;
   }
   ++c->gen;
   c->attr = 0;      // the dynamic-LDS opt-ins are per kernel, and the kernels depend on K
@@ -1737,8 +1746,11 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   // batch; MMSBM_UNITS="a,b" overrides them (tests: tiny units force every split path).  The fused
   // small-K launch packs full units (as few as the chunk cap allows: the grid must be resident).
   int units_a = 1536, units_b = 3072;
+  int ncu = 0;
   if (c->sk_fused) {  // about the waves resident at once: 15 per CU (two 8-wave workgroups, some
-    int ncu = 0;      // headroom for units the stretch cap or a section's end leave short)
+                      // headroom for units the stretch cap or a section's end leave short).  The
+                      // unit length sets the sums' order: bits depend on the device's CU count
+                      // (plan_info[12]), not on B or the rank
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu < 1)
       ncu = 256;
     units_a = units_b = 15 * ncu;
@@ -1756,6 +1768,8 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
                            c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, 1024, c->sk_fused,
                            mmsbm_plan::sk_gu(c->K), rho);
   const auto& h = sd.h;
+  sd.ncu = c->sk_fused ? ncu : 0;
+  sd.unit_target = c->sk_fused ? units_a : 0;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;
   if ((rc = upload(&sd.chunk_vslot, h.chunk_vslot))) return rc;
@@ -2073,6 +2087,9 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[8] = h.small ? info[9] : (int64_t)h.vgenes.size();  // small-K: one V table per stream-0 stretch
   info[10] = h.small ? (c->sk_fused ? 2 : 1) : 0;
   info[11] = h.small ? h.n_units : (int64_t)(h.n_wg_a + h.n_wg_b) * NW;
+  info[12] = c->sets[which].ncu;
+  info[13] = c->sets[which].unit_target;
+  info[14] = info[15] = 0;
   return MMSBM_OK;
 }
 

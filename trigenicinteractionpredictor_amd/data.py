@@ -93,10 +93,17 @@ def _python_triples(spec: FoldSpec, rng: random.Random):
 
 
 def _numpy_triples(spec: FoldSpec):
-    """Vectorised variant for large E (10M-link stress config)."""
+    """Vectorised variant for large E (10M-link stress config).  Takes the hub options (the
+    same rule as the Python path: hub_share of the drawn triples take their first gene from the
+    first hub_frac of the permutation); the per-line options (multi / both / dup) belong to the
+    Python path only and raise here."""
     P, E = spec.P, spec.E
+    if spec.multi_frac or spec.both_frac or spec.dup_frac:
+        raise NotImplementedError("multi_frac / both_frac / dup_frac: only for E < 1,000,000 "
+                                  "(the per-line Python generator)")
     rs = np.random.default_rng(spec.seed)
     perm = rs.permutation(P)
+    hubs = perm[: max(1, int(P * spec.hub_frac))] if spec.hub_frac else None
     nfull = P // 3
     cover = np.sort(perm[: nfull * 3].reshape(nfull, 3), axis=1)
     if P % 3:
@@ -110,6 +117,9 @@ def _numpy_triples(spec: FoldSpec):
     while codes.size < need:
         m = int((need - codes.size) * 1.1) + 1024
         t = rs.integers(0, P, size=(m, 3))
+        if hubs is not None:      # (no extra draws without hubs: the uniform folds are unchanged)
+            hub = rs.random(m) < spec.hub_share
+            t[hub, 0] = hubs[rs.integers(0, hubs.size, size=int(hub.sum()))]
         t = t[(t[:, 0] != t[:, 1]) & (t[:, 0] != t[:, 2]) & (t[:, 1] != t[:, 2])]
         t.sort(axis=1)
         c = np.unique(enc(t))

@@ -74,11 +74,11 @@ class EMEngine:
         _lib.check(self.lib.mmsbm_set_workspace(self.ctx, _ptr(self.workspace), self.workspace.numel()))
 
     def plan_info(self, which: int = _lib.SET_TRAIN) -> dict:
-        v = (ctypes.c_int64 * 12)()
+        v = (ctypes.c_int64 * 16)()
         _lib.check(self.lib.mmsbm_plan_info(self.ctx, which, v))
         keys = ("observations", "rows", "rows_stream0", "wg_stream0", "wg_stream12", "wg_spartial",
                 "partial_rows", "genes_per_wg_max", "v_genes", "partial_rows_stream0", "small_k",
-                "units")
+                "units", "plan_cus", "unit_target")
         return dict(zip(keys, [int(x) for x in v]))
 
     # ------------------------------------------------------------ parameters

@@ -32,7 +32,7 @@ import numpy as np
 
 from . import _lib
 from .layout import links_to_arrays
-from .tracked import TrackedTable, version_of
+from .tracked import TrackedLinks, TrackedTable, version_of
 
 HO_DELTA = "hoΔ"   # the filler allele removed from every key (:318-323, :405-410)
 
@@ -262,9 +262,27 @@ class Model:
     del _param
 
     def links_changed(self):
-        """Declare an edit of the link dicts: the device tables are rebuilt on the next call
-        (the reference re-reads the dicts on every call)."""
+        """Declare an edit of the link dicts the tables cannot see (a key added to or removed
+        from a dict assigned to `links` / `dlinks`; tracked.TrackedLinks): the tables re-read
+        their source dicts and the device tables are rebuilt on the next call (the reference
+        re-reads the dicts on every call)."""
+        for t in (self.links, self.dlinks):
+            t.resync()
         self._engine_key = None
+
+    # copy.deepcopy / pickle: no device engine in the copy, tables tracked again
+    def __getstate__(self):
+        self._pull()
+        state = dict(self.__dict__)
+        state.update(_engine=None, _engine_key=None, _dev_fresh=False, _host_fresh=True)
+        return state
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        for name in ("_tracked_links", "_tracked_dlinks"):
+            t = self.__dict__.get(name)
+            if t is not None and not isinstance(t, TrackedLinks):
+                self.__dict__[name] = TrackedLinks(t)
 
     def _ensure_engine(self):
         key = (self.K, self.P, version_of(self.links), version_of(self.dlinks))

@@ -70,8 +70,10 @@ class LinkShardedEM:
         self.device = engine.device
 
     def _sum(self, t):
-        """Sum over ranks in place (one collective); gloo reduces a host copy."""
-        if self.world == 1:
+        """Sum over ranks in place (one collective, also in a world of one when a process group
+        exists: bench.py --process-group runs the RCCL all-reduce on one GPU); gloo reduces a host
+        copy."""
+        if not self.dist_on:
             return t
         import torch.distributed as dist
         if t.is_cuda and dist.get_backend(self.group) == "gloo":
@@ -98,7 +100,7 @@ class LinkShardedEM:
     def loglik(self, which: int = TRAIN) -> np.ndarray:
         import torch
         local = torch.as_tensor(np.asarray(self.engine.loglik(which), dtype=np.float64))
-        if self.world > 1 and getattr(self.buf, "is_cuda", False):
+        if self.dist_on and getattr(self.buf, "is_cuda", False):
             import torch.distributed as dist
             if dist.get_backend(self.group) != "gloo":
                 local = local.to(self.buf.device)

@@ -23,7 +23,7 @@ import numpy as np
 
 from . import _lib
 from .layout import links_to_arrays
-from .tracked import TrackedLinks, version_of
+from .tracked import TrackedLinks, tracked, version_of
 
 
 NATIVE_INGEST = True   # get_traintest's native reader for canonical files (ingest.py)
@@ -107,7 +107,9 @@ class Model:
 
     @links.setter
     def links(self, value):
-        self._links = value if isinstance(value, TrackedLinks) else TrackedLinks(value)
+        # a plain dict is aliased, not copied (tracked.TrackedLinks): `m.links = d` then
+        # `d[k][r] += 1` reaches the device like the reference's shared object would
+        self._links = tracked(value)
         self._fold_v[0] = None
 
     @property
@@ -119,7 +121,7 @@ class Model:
 
     @test_links.setter
     def test_links(self, value):
-        self._test_links = value if isinstance(value, TrackedLinks) else TrackedLinks(value)
+        self._test_links = tracked(value)
         self._fold_v[1] = None
 
     @property
@@ -133,9 +135,30 @@ class Model:
         self._nlinks = value
 
     def links_changed(self):
-        """Declare an edit the tables cannot see (e.g. of a dict object kept from before it was
-        assigned to `links`): the device tables are rebuilt on the next call."""
+        """Declare an edit the tables cannot see: a key added to or deleted from a dict that was
+        assigned to `links` / `test_links` (row edits such as `d[k][1] += 1` are seen without
+        it).  The tables re-read their source dicts and the device copy is rebuilt on the next
+        call."""
+        for t in (self._links, self._test_links):
+            if isinstance(t, TrackedLinks):
+                t.resync()
         self._links_version += 1
+
+    # copy.deepcopy / pickle: the device engine is not copied (the copy builds its own on first
+    # use, from freshly pulled host parameters) and the tables come back tracked
+    def __getstate__(self):
+        self._pull()
+        state = dict(self.__dict__)
+        state.update(_engine=None, _engine_key=None, _dev_fresh=False, _host_fresh=True)
+        return state
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        for name in ("_links", "_test_links"):
+            t = self.__dict__.get(name)
+            if t is not None and not isinstance(t, TrackedLinks):
+                # (a new version: _fold_fresh then reads the copied table, not the parse)
+                self.__dict__[name] = TrackedLinks(t)
 
     def _fold_fresh(self, which):
         """The parsed arrays still hold table `which` (nothing edited or replaced it)."""

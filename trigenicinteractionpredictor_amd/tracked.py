@@ -100,14 +100,39 @@ class TrackedRow(list):
 
 class TrackedLinks(dict):
     """`links` / `test_links`: key 'i_j_k' -> TrackedRow of counts.  Any edit of the table or of
-    one of its rows bumps `version.n`."""
+    one of its rows bumps `version.n`.
 
-    def __init__(self, src=None, version: Version = None):
+    `alias`: a plain dict the caller assigned (`model.links = d`).  The reference stores that very
+    object, so later edits of `d` are edits of `model.links`.  A dict cannot be made to notice its
+    own edits, so the table keeps `d` as its source and shares the row objects with it: `d`'s
+    values are replaced by the table's TrackedRow rows (equal lists), so `d[k][r] += 1` is seen at
+    once; every edit made through the table is applied to `d` too; and a key added to or removed
+    from `d` itself is picked up by `resync()` (what `Model.links_changed()` calls)."""
+
+    def __init__(self, src=None, version: Version = None, alias: dict = None):
         super().__init__()
         self.version = version if version is not None else Version()
+        self.src = alias
+        if alias is not None:
+            src = alias
         if src:
-            for k, v in (src.items() if hasattr(src, "items") else src):
-                dict.__setitem__(self, k, self._row(v))
+            for k, v in (list(src.items()) if hasattr(src, "items") else src):
+                row = self._row(v)
+                dict.__setitem__(self, k, row)
+                if alias is not None and row is not v:
+                    alias[k] = row
+
+    def resync(self):
+        """Re-read the aliased source dict (edits made to it directly); no-op without one."""
+        if self.src is None:
+            return
+        dict.clear(self)
+        for k, v in list(self.src.items()):
+            row = self._row(v)
+            dict.__setitem__(self, k, row)
+            if row is not v:
+                self.src[k] = row
+        self.version.bump()
 
     def _row(self, v):
         if isinstance(v, list):
@@ -117,11 +142,16 @@ class TrackedLinks(dict):
         return v
 
     def __setitem__(self, k, v):
-        dict.__setitem__(self, k, self._row(v))
+        row = self._row(v)
+        dict.__setitem__(self, k, row)
+        if self.src is not None:
+            self.src[k] = row
         self.version.bump()
 
     def __delitem__(self, k):
         dict.__delitem__(self, k)
+        if self.src is not None:
+            self.src.pop(k, None)
         self.version.bump()
 
     def setdefault(self, k, default=None):
@@ -132,7 +162,10 @@ class TrackedLinks(dict):
 
     def update(self, *a, **kw):
         for k, v in dict(*a, **kw).items():
-            dict.__setitem__(self, k, self._row(v))
+            row = self._row(v)
+            dict.__setitem__(self, k, row)
+            if self.src is not None:
+                self.src[k] = row
         self.version.bump()
 
     def __ior__(self, other):
@@ -141,20 +174,36 @@ class TrackedLinks(dict):
 
     def pop(self, *a):
         r = dict.pop(self, *a)
+        if self.src is not None and a:
+            self.src.pop(a[0], None)
         self.version.bump()
         return r
 
     def popitem(self):
-        r = dict.popitem(self)
+        k, v = dict.popitem(self)
+        if self.src is not None:
+            self.src.pop(k, None)
         self.version.bump()
-        return r
+        return k, v
 
     def clear(self):
         dict.clear(self)
+        if self.src is not None:
+            self.src.clear()
         self.version.bump()
 
     def __reduce_ex__(self, protocol):   # pickles / deep-copies as a plain dict of lists
         return (dict, ({k: list(v) if isinstance(v, list) else v for k, v in self.items()},))
+
+
+def tracked(value):
+    """The table a Model stores for an assigned value: a TrackedLinks as is, None as is (not
+    materialised), any other mapping as a TrackedLinks aliasing it."""
+    if value is None or isinstance(value, TrackedLinks):
+        return value
+    if isinstance(value, dict):
+        return TrackedLinks(alias=value)
+    return TrackedLinks(value)
 
 
 def version_of(table) -> int:
@@ -164,7 +213,7 @@ def version_of(table) -> int:
 
 class TrackedTable:
     """Class attribute that keeps a TrackedLinks in the instance: assigning a plain dict stores a
-    tracked copy of it (a new table, with a new version)."""
+    table aliasing it (`tracked`), with a new version."""
 
     def __set_name__(self, owner, name):
         self.slot = "_tracked_" + name
@@ -175,4 +224,4 @@ class TrackedTable:
         return obj.__dict__[self.slot]
 
     def __set__(self, obj, value):
-        obj.__dict__[self.slot] = value if isinstance(value, TrackedLinks) else TrackedLinks(value)
+        obj.__dict__[self.slot] = tracked(value)
