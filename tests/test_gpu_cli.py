@@ -56,3 +56,33 @@ def test_cli_batch_mode_on_gpu_matches_reference_loop(tmp_path):
             want = float([l for l in got if l.startswith("Sample %d:" % s)][0].split()[5])
             np.testing.assert_allclose(like, want, rtol=1e-12)
             assert "Held-out Likelihood:\t" in text and "\nTest set:\n" in text
+
+
+def test_cli_gpus_2_on_one_gpu_writes_the_batch_files(tmp_path):
+    """`--gpus 2 --backend gloo` (the command spawns its two ranks before any GPU call; on this
+    one-GPU box both share cuda:0) writes the same Sample files, byte for byte, as one process
+    with `--batch 2`: a sample's bits depend neither on its batch nor on its rank, and rank 0
+    prints every sample's summary (src/run.sh:36-45, :1253-1279)."""
+    import subprocess
+    import sys
+    one, two = tmp_path / "one", tmp_path / "two"
+    one.mkdir()
+    two.mkdir()
+    base = ["-k", "3", "-i", "60", "-n", "4", "-f", "4", "-b", "6", "-t", TRAIN, "-e", TEST, "--seed", "7"]
+    with contextlib.redirect_stdout(io.StringIO()):
+        rc = cli.main(base + ["-o", str(one) + os.sep, "--batch", "2"], out=lambda *_: None)
+    assert rc == 0
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-m", "trigenicinteractionpredictor_amd.cli", *base,
+                        "-o", str(two) + os.sep, "--batch", "2", "--gpus", "2", "--backend", "gloo"],
+                       cwd=repo, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    files = sorted(os.listdir(one))
+    assert files and files == sorted(os.listdir(two))
+    for f in files:
+        assert (one / f).read_bytes() == (two / f).read_bytes(), f
+    summary = [l for l in p.stdout.splitlines() if l.startswith("Sample ") and "iterations" in l]
+    assert [int(l.split()[1][:-1]) for l in summary] == [0, 1, 2, 3]
