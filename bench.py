@@ -115,18 +115,20 @@ def spawn_ranks(n):
     return rc
 
 
-KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, d, c, M0 on FP64 MFMA)",
+KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, Z', d, c, the j / k Y entries, M0 "
+                          "partial rows; FP64 MFMA)",
+                "gene": "gene_kernel<%d> (X0 contractions on FP64 MFMA, S partials, Y entry sums)",
                 "fused": "sk_pass_kernel<%d, SK_U> (fused E-step, all 3 streams: V, Z, d, c, M, X; "
                          "stream-0 S partials; FP64 MFMA)",
-                "pass_b": "pass_kernel<%d, PASS_B> (streams 1/2: M1, M2; S partials)",
-                "fin": "fin_kernel<%d> (per-gene X contractions, theta and p update)"}
+                "pass_b": "sk_pass_kernel<%d, SK_B> (streams 1/2: M1, M2, X)",
+                "fin": "fin: sk_fin_kernel<%d> / upd_kernel (theta and p update)"}
 
 
 def kernel_work(plan, K, P, R, B, E_obs):
-    """Algorithmic (FLOPs, HBM bytes) of one launch of each kernel of the pivot-run iteration
-    (DESIGN.md "Roofline accounting"): per observation 2K^2 (Z) + 2K (d) + 2K^2 (M) in pass A,
-    2 x 2K^2 (M1, M2) in pass B; per pivot gene 2K^3 (V, S partial, each X); bytes = the
-    records, c, partial rows and parameters each launch must move once."""
+    """Algorithmic (FLOPs, HBM bytes) of one launch of each kernel of the iteration, keyed by the
+    engine's kernel labels (EMEngine.LABELS; DESIGN.md "Roofline accounting"): per observation
+    2K^2 per K^2 contraction (Z, Z', M) and 2K (d); per pivot-gene table or contraction 2K^3;
+    bytes = the records, Y entries, partial rows and parameters each launch must move once."""
     K2, K3 = K * K, K ** 3
     rows0, rows = plan["rows_stream0"], plan["rows"]
     prows = plan["partial_rows"]
@@ -142,7 +144,7 @@ def kernel_work(plan, K, P, R, B, E_obs):
         u_by = 16.0 * rows + 8.0 * K * prows + 8.0 * K3 * wga + params
         f_fl = 1.0 * prows * K + R * K3 * wga + 3.0 * P * K + 3.0 * R * K3
         f_by = 8.0 * K * prows + 8.0 * K3 * wga + 2 * params + 4.0 * 6 * P
-        return {"pass_a": (u_fl * B, u_by * B), "pass_b": (0.0, 0.0), "fin": (f_fl * B, f_by * B)}
+        return {"fused": (u_fl * B, u_by * B), "fin": (f_fl * B, f_by * B)}
     if plan.get("small_k"):
         # small-K kernels (csrc/sk.h): per stream-0 stretch a V table, an X contraction and an S
         # update (2K^3 each); per stream-1/2 stretch an X contraction; bytes: records, row12 and
@@ -155,13 +157,22 @@ def kernel_work(plan, K, P, R, B, E_obs):
         f_fl = 1.0 * prows * K + R * K3 * wga + 3.0 * P * K + 3.0 * R * K3
         f_by = 8.0 * K * prows + 8.0 * K3 * wga + 2 * params + 4.0 * 6 * P
         return {"pass_a": (a_fl * B, a_by * B), "pass_b": (b_fl * B, b_by * B), "fin": (f_fl * B, f_by * B)}
-    a_fl = E_obs * (4.0 * K2 + 2.0 * K) + genes_a * 2.0 * K3
-    a_by = 16.0 * rows0 + 8.0 * rows0 + 8.0 * K2 * prow0 + params
-    b_fl = E_obs * 4.0 * K2 + prow0 * 2.0 * K3
-    b_by = 16.0 * (rows - rows0) + 8.0 * (rows - rows0) + 8.0 * K2 * prows + params
-    f_fl = 3.0 * R * P * 2.0 * K3 + 3.0 * R * K3
-    f_by = 8.0 * K2 * prows + 2.0 * params
-    return {"pass_a": (a_fl * B, a_by * B), "pass_b": (b_fl * B, b_by * B), "fin": (f_fl * B, f_by * B)}
+    # large-K kernels (csrc/mmsbm.hip): pass A per observation Z, Z', M (2K^2 each) + d, per
+    # workgroup gene a V table; it reads the records + their Y entry indices and writes 2K words
+    # of Y entries per observation and the K^2 stream-0 partial rows.  The gene kernel: per
+    # (gene, rating) with stream-0 rows an X0 contraction (2K^3; at most P R), per partial row an
+    # S update (2K^3), per Y entry K adds; it reads the partial rows twice and the Y entries once,
+    # writes x0, ysum and the S partials.  The update: theta from x0 + ysum, p from the S partials.
+    n_sp = plan["wg_spartial"]
+    n_y = plan.get("y_entries", 2 * E_obs)
+    xg = min(P * R, prow0)
+    a_fl = E_obs * (6.0 * K2 + 2.0 * K) + genes_a * 2.0 * K3
+    a_by = 16.0 * rows0 + 8.0 * rows0 + 8.0 * K * n_y + 8.0 * K2 * prow0 + params
+    g_fl = xg * 2.0 * K3 + prow0 * 2.0 * K3 + n_y * K
+    g_by = 2 * 8.0 * K2 * prow0 + 8.0 * K * n_y + 8.0 * K3 * n_sp + 2 * 8.0 * P * K + params
+    f_fl = 3.0 * P * K + n_sp * R * K3 + 3.0 * R * K3
+    f_by = 3 * 8.0 * P * K + 8.0 * K3 * n_sp + 2 * params
+    return {"pass_a": (a_fl * B, a_by * B), "gene": (g_fl * B, g_by * B), "fin": (f_fl * B, f_by * B)}
 
 
 def s8d_work(K, P, R, B, E_obs):
@@ -232,8 +243,7 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
             "hbm": {"bytes_per_iteration": b8, "achieved": b8 / iter_s / 1e9, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": b8 / iter_s / 1e9 / HBM_PEAK_GBS,
                     "traffic_over_compulsory": None if traffic is None else traffic / b8},
-            "dominant_kernel": {"kernel": KERNEL_NAMES["fused" if plan.get("small_k") == 2 and dom == "pass_a"
-                                                    else dom] % K, "avg_launch_us": dom_s * 1e6,
+            "dominant_kernel": {"kernel": KERNEL_NAMES[dom] % K, "avg_launch_us": dom_s * 1e6,
                                 "executed_flops_per_launch": dfl, "algorithmic_bytes_per_launch": dby,
                                 "tflops": dfl / dom_s / 1e12, "mfma_frac": dfl / dom_s / 1e12 / FP64_PEAK_TFLOPS,
                                 "gbs": dby / dom_s / 1e9, "hbm_frac": dby / dom_s / 1e9 / HBM_PEAK_GBS,
@@ -433,7 +443,8 @@ def main():
     eng.timing(0 if args.no_events else args.event_stride)
     runner.iterate(args.warmup - first_w)
     torch.cuda.synchronize(dev)
-    in_loop = {k: eng.timing_result(k) for k in eng.KERNELS}
+    labels = eng.kernels()
+    in_loop = {k: eng.timing_result(k) for k in labels}
     eng.timing(False)
     if dist_on:
         dist.barrier()
@@ -446,8 +457,7 @@ def main():
         dist.barrier()
     # each kernel of the iteration alone, back to back on the launch stream (per-launch duration
     # for the roofline; the in-loop events above also time the dependent-launch boundary)
-    launched = eng.launched_kernels()
-    b2b = {k: eng.time_kernel(k, args.roofline_launches) for k in launched}
+    b2b = {k: eng.time_kernel(k, args.roofline_launches) for k in labels}
     elapsed = t1 - t0
     L = runner.loglik(0)
     rows = result_rows(sample_ids, L)
@@ -508,12 +518,11 @@ def main():
             "build_id": build_id,
             "roofline": roofline,
             "iteration": {"us": iter_s * 1e6},
-            # kernels the iteration does not launch (the fused small-K E-step has no pass B) are
-            # null: their event pairs would only time the events themselves
-            "kernel_us": {k: ({"back_to_back": b2b[k] * 1e3,
-                               "in_loop": in_loop[k][0] * 1e3 / max(in_loop[k][1], 1)}
-                              if k in launched else None)
-                          for k in eng.KERNELS},
+            # the kernels the iteration launches (EMEngine.kernels(): the fused small-K E-step
+            # has no pass B, the large-K iteration runs pass A, the gene kernel and the update)
+            "kernel_us": {k: {"back_to_back": b2b[k] * 1e3,
+                              "in_loop": in_loop[k][0] * 1e3 / max(in_loop[k][1], 1)}
+                          for k in labels},
             "plan": plan,
             "cpu_baseline": cpu_rec,
         }

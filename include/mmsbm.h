@@ -123,19 +123,22 @@ int mmsbm_mstep(mmsbm_ctx *ctx, double *theta, double *pr, const double *nth, co
  * mmsbm_accumulate.  The pointer is read at every launch; it stays set until replaced. */
 int mmsbm_set_theta_addend(mmsbm_ctx *ctx, const double *nth_add);
 
-/* Measurement: info[16] = observations, plan rows (3 streams), stream-0 rows, stream-0
- * workgroups, stream-1/2 workgroups, S partials, partial rows, most genes per stream-0
- * workgroup (per unit for the small-K plan), V tables computed per iteration, stream-0 partial
- * rows, 1 if the plan is the small-K one (K <= 12, sk.h; 2: with the fused E-step launch, pass A
- * then runs all three streams and pass B is empty), units (waves of work), [12] the compute-unit
- * count the fused plan sized its units from (0: the plan does not depend on it), [13] that plan's
- * unit target, [14], [15] reserved (0).  The fused plan's unit length, and so the order of its
- * sums, follows [12]: results are bitwise reproducible on one device model / partition mode. */
+/* Measurement: info[16] = observations, plan rows (3 streams on the small-K plans, stream 0 on the
+ * large-K ones), stream-0 rows, stream-0 workgroups, stream-1/2 workgroups, S partials, partial
+ * rows, most genes per stream-0 workgroup (per unit for the small-K plan), V tables computed per
+ * iteration, stream-0 partial rows, 1 if the plan is the small-K one (K <= 12, sk.h; 2: with the
+ * fused E-step launch, pass A then runs all three streams and pass B is empty; 0: the large-K
+ * kernels), units (waves of work), [12] the compute-unit count the fused plan sized its units
+ * from (0: the plan does not depend on it), [13] that plan's unit target, [14] Y entries of the
+ * large-K plan (2 per observation), [15] reserved (0).  The fused plan's unit length, and so the
+ * order of its sums, follows [12]: results are bitwise reproducible on one device model /
+ * partition mode. */
 int mmsbm_plan_info(const mmsbm_ctx *ctx, int32_t which, int64_t *info);
 
 /* Kernel timing for measurement (bench.py): with stride n > 0, mmsbm_iterate records a HIP
  * event pair on the launch stream around every kernel of every n-th iteration (kernel ids:
- * 0 pass A = stream 0, 1 pass B = streams 1/2 + S partials, 2 fin = theta / p update);
+ * 0 = pass A (large-K: stream 0 + Y entries; fused small-K: the whole E-step), 1 = the large-K
+ * gene kernel (x0, S partials, Y sums) / the small-K pass B, 2 = fin (theta / p update));
  * 0 disables.  mmsbm_timing resets the counters; mmsbm_timing_result waits for the last event
  * and returns the summed device time (ms) and the number of timed launches of that kernel. */
 int mmsbm_timing(mmsbm_ctx *ctx, int32_t stride);

@@ -168,8 +168,9 @@ int main() {
     }
   }
 
-  // 1. every observation appears once per stream, with its count on stream 0 and its stream-0
-  //    row on streams 1 / 2; padding rows carry a zero count / the zero c slot
+  // 1. every observation appears once per stream (small-K plans: 3 streams; large-K: stream 0),
+  //    with its count on stream 0 and its stream-0 row on streams 1 / 2; padding rows carry a zero
+  //    count / the zero c slot
   long long n_obs = 0;
   for (long long e = 0; e < E; ++e)
     for (int r = 0; r < R; ++r) n_obs += counts[e * R + r] > 0;
@@ -276,6 +277,35 @@ int main() {
       at = pl.sp_desc[3 * sp + 2];
     }
     if (q1 > q0 && at != q1) return fail("sp end", r, at);
+  }
+  // 6. large-K EM plans hold stream 0 only; Y entries: yptr tiles [0, n_y = 2 x observations),
+  //    an entry of gene g's range is named by exactly one (stream-0 row, slot 1 / 2) whose slot gene
+  //    is g, and padding rows name the dummy entry n_y
+  if (pl.n_wg_b != 0 || (long long)pl.rows.size() != pl.n_rows0) return fail("large-K streams", pl.n_wg_b);
+  if (pl.n_y != 2 * n_obs || (int)pl.yptr.size() != P + 1 || pl.yptr[0] != 0 || pl.yptr[P] != pl.n_y)
+    return fail("yptr", pl.n_y, 2 * n_obs);
+  if ((long long)pl.row_y.size() != 2 * pl.n_rows0) return fail("row_y size");
+  {
+    std::vector<int> owner(pl.n_y, -1), hits(pl.n_y, 0);
+    for (int g = 0; g < P; ++g) {
+      if (pl.yptr[g + 1] < pl.yptr[g]) return fail("yptr order", g);
+      for (int e = pl.yptr[g]; e < pl.yptr[g + 1]; ++e) owner[e] = g;
+    }
+    for (long long q = 0; q < pl.n_rows0; ++q) {
+      const I4& x = pl.rows[q];
+      for (int k = 0; k < 2; ++k) {
+        const int e = pl.row_y[2 * q + k];
+        if (x.w <= 0) {
+          if (e != pl.n_y) return fail("row_y padding", q, e);
+          continue;
+        }
+        if (e < 0 || e >= pl.n_y) return fail("row_y range", q, e);
+        if (owner[e] != (k == 0 ? x.y : x.z)) return fail("row_y gene", q, e);
+        hits[e]++;
+      }
+    }
+    for (long long e = 0; e < pl.n_y; ++e)
+      if (hits[e] != 1) return fail("y entry coverage", e, hits[e]);
   }
   printf("ok %zu %d %d %lld %d\n", pl.rows.size(), n_wg * NW, n_wg, pl.n_prows, pl.n_sp);
   return 0;

@@ -11,9 +11,9 @@ import glob
 import json
 import sys
 
-NAMES = {"pass_kernel<%d, 0>": "pass_a", "pass_kernel<%d, 2>": "pass_b", "fin_kernel<%d, false>": "fin",
-         # small-K kernels (csrc/sk.h): the fused E-step is the iteration's "pass_a"
-         "sk_pass_kernel<%d, 3>": "pass_a", "sk_pass_kernel<%d, 0>": "pass_a",
+NAMES = {"pass_kernel<%d, 0>": "pass_a", "gene_kernel<%d>": "gene", "upd_kernel<%d, false>": "fin",
+         # small-K kernels (csrc/sk.h), labelled as EMEngine.LABELS names them
+         "sk_pass_kernel<%d, 3>": "fused", "sk_pass_kernel<%d, 0>": "pass_a",
          "sk_pass_kernel<%d, 2>": "pass_b", "sk_fin_kernel<%d, false>": "fin"}
 
 

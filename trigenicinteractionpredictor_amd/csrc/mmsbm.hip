@@ -194,10 +194,10 @@ __device__ __forceinline__ double row16_sum(double v) {
   return v;
 }
 
-enum { PASS_A = 0, PASS_LL = 1, PASS_B = 2 };
+enum { PASS_A = 0, PASS_LL = 1, PASS_B = 2 };  // (PASS_B: the small-K family's stream-1/2 pass)
 
 // ------------------------------------------------------------------------------------------
-// S partial of one workgroup (launch B): S_r[a][cell] += th_g(q)[a] M_q[cell] over the partial rows
+// S partial of one workgroup (gene_kernel): S_r[a][cell] += th_g(q)[a] M_q[cell] over the partial rows
 // q of stream 0, rating r, in [q0, q1), cells (b, h) dense.  MFMA k index = four partial rows,
 // blocks = four cell tiles; wave wv of item group ig owns cell group cg = ig NW + wv (16 cells)
 // for every a tile, so each partial-row value is loaded once and feeds NG MFMAs.
@@ -265,24 +265,25 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
 }
 
 // ------------------------------------------------------------------------------------------
-// Pass kernel, grid (workgroups, B), block 512 = one unit (contiguous chunks) per wave.
-// MODE PASS_A / PASS_LL: stream-0 workgroups; PASS_B: stream 1/2 workgroups, then S-partial ones.
+// Pass kernel, grid (workgroups, B), block 512 = one unit (contiguous chunks) per wave; stream 0
+// only (the plan's large-K layout, plan.h).  MODE PASS_A: the EM E-step; PASS_LL: the likelihood.
 // MFMA lane map (v_mfma_f64_4x4x4f64, lane = 16 hi + 4 blk + lo): A[blk][m = lo][k = hi],
 // B[blk][k = hi][n = lo], D[blk][m = hi][n = lo] (tools/micro/mfma_layout.hip).
 //   Z   (blocks = b tiles, k = h):  A = th_v[obs lo][4 hs + hi], B = V_g[b][4 hs + hi]  -> Z[obs hi][b]
-//   M   (blocks = (x, y) tiles, k = the chunk's 4 observations):
-//       A = th_u[obs hi][x], B = c_o th_v[obs hi][y]  -> M[x = 4 xs + hi][y = 4 ys + lo]
+//   Z'  (blocks = h tiles, k = b):  A = th_u[obs lo][4 bs + hi], B = V_g[4 bs + hi][h] -> Z'[obs hi][h]
+//   M   (v_mfma_f64_16x16x4, k = the chunk's 4 observations): M[x][y] += c th_u[x] th_v[y]
+// Per observation (u = j, v = k; src/TrigenicInteractionPredictor.py:996-1012):
+//   d = eps + th_j . Z,  c = n / d,  Y[entry j] = c Z  (= ntheta_j / th_j),  Y[entry k] = c Z'
+// and per gene stretch the M^0 partial row (K^2) for X^0 and S (gene_kernel).
 // ------------------------------------------------------------------------------------------
 template <int K, int MODE>
 __global__ __launch_bounds__(NT) void pass_kernel(
     const int4* __restrict__ rows, const int* __restrict__ chunk_prow,
-    const int* __restrict__ chunk_vslot, const int* __restrict__ wg_units,
+    const int* __restrict__ chunk_vslot, const int* __restrict__ row_y, const int* __restrict__ wg_units,
     const int* __restrict__ wg_code, const int* __restrict__ wg_gene, const int* __restrict__ vgenes,
-    const int* __restrict__ sp_desc, const int* __restrict__ prow_gene,
-    const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ cbuf,
-    double* __restrict__ prows, double* __restrict__ spart, double* __restrict__ pold,
-    double* __restrict__ partL, int P, int R, long long n_rows0, long long n_prows, int n_wg,
-    int n_sp, double eps, int gcap) {
+    const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ ybuf,
+    double* __restrict__ prows, double* __restrict__ partL, int P, int R, long long n_y,
+    long long n_prows, int n_wg, double eps, int gcap) {
   using T = KT<K>;
   constexpr int NG = T::NG, TR = T::TR, VR = T::VR;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -295,47 +296,34 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   st_.mark(0);
   const long long wave_id = ((long long)b * gridDim.x + w) * NW + wv;
 
-  if constexpr (MODE == PASS_B) {
-    if (w >= n_wg) {  // S partial + snapshot of p for fin_kernel (which updates p in place)
-      const int sw = w - n_wg, sp = sw / T::NIG, ig = sw % T::NIG;
-      const int* d = sp_desc + 3 * sp;
-      s_partial<K>(th, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
-                   spart + ((size_t)b * n_sp + sp) * T::K3, smem, ig, tid, wv, hi, blk, lo, st_);
-      const long long tot = (long long)R * T::K3, nsw = (long long)n_sp * T::NIG;
-      const long long c0 = tot * sw / nsw, c1 = tot * (sw + 1) / nsw;
-      for (long long idx = c0 + tid; idx < c1; idx += NT)
-        st_wt(pold + (size_t)b * tot + idx, pr[(size_t)b * tot + idx]);
-      st_.mark(3);
-      st_.flush(3, wave_id, lane);
-      return;
-    }
-  }
-
   const int code = wg_code[w];
-  const int s = code >> 4, r = code & 15;
+  const int r = code & 15;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * T::K3;
   double* Vt = smem;
   // LDS: [gcap V tables][gcap theta rows][per-wave images]; gcap (<= GMAX) = the plan's most
-  // genes per stream-0 workgroup
-  double* Tg = smem + (MODE == PASS_B ? 0 : gcap * T::VDBL);  // theta rows of the V genes
-  double* img = smem + (MODE == PASS_B ? 0 : gcap * (T::VDBL + T::KP)) + wv * T::IMGW;
+  // genes per workgroup
+  double* Tg = smem + gcap * T::VDBL;  // theta rows of the V genes
+  double* img = smem + gcap * (T::VDBL + T::KP) + wv * T::IMGW;
 
   // this wave's unit, and the first records of its pipeline (in flight during the V prologue).
   // Record stream: lane l < 16 holds int l of the chunk's 4 records (i, j, k, w), lane 16 the
-  // chunk's partial row, lane 17 its V slot; the other lanes read them by readlane / shuffle, so
-  // no register array is indexed at run time.
+  // chunk's partial row, lane 17 its V slot, lanes 18-25 the 4 rows' Y entries (slot 1, slot 2);
+  // the other lanes read them by readlane / shuffle, so no register array is indexed at run time.
   // Ring of U record registers: the loop below is unrolled U times so each ring slot keeps a
   // fixed register (a rotation by register moves would wait for every load in flight).
   constexpr int U = 6;   // records U - 1 chunks ahead
-  constexpr int DT = 2;  // theta values and c DT chunks ahead (ring of U slots, DT + 1 live)
+  constexpr int DT = 2;  // theta values DT chunks ahead (ring of U slots, DT + 1 live)
+  constexpr bool EM = MODE == PASS_A;
   const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
   const int* __restrict__ rows_i = reinterpret_cast<const int*>(rows);
   // Every load in the chunk loop is issued by every lane on every path (addresses clamped, values
   // selected afterwards): an exec-masked load behind a branch would make the compiler's vmcnt
   // accounting assume it may be missing and wait for everything in flight.
   const int lr = lane & 31;  // this lane's record word: base and stride fixed once
-  const int* __restrict__ rbase = lr < 16 ? rows_i + lr : lr == 16 ? chunk_prow : chunk_vslot;
-  const int rstride = lr < 16 ? 16 : 1;
+  const bool ylane = EM && lr >= 18 && lr < 26;
+  const int* __restrict__ rbase = lr < 16 ? rows_i + lr : lr == 16 ? chunk_prow : lr == 17 ? chunk_vslot
+                                  : ylane ? row_y + (lr - 18) : rows_i;
+  const int rstride = lr < 16 ? 16 : lr < 18 ? 1 : ylane ? 2 * CH : 16;
   auto ld_rec = [&](int q) -> int { return rbase[(size_t)q * rstride]; };
   auto clampq = [&](int q) { return q < c1 ? q : c1 - 1; };
   const bool any = c0 < c1;
@@ -344,7 +332,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   for (int i = 0; i < U - 1; ++i) rv[i] = any ? ld_rec(clampq(c0 + i)) : 0;
   rv[U - 1] = 0;
 
-  if constexpr (MODE != PASS_B) {
+  {
     // ---- V_g[b][h] = sum_a th_g[a] p_r[a][b][h] for the workgroup's pivot genes (LDS)
     // vgenes holds GMAX (padded) genes per workgroup, so the theta loads do not wait for
     // wg_gene; p_r is staged in the image region when it fits.  All loads go out together.
@@ -440,13 +428,10 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   }
   st_.mark(1);
 
-  double* __restrict__ cb = cbuf + (size_t)b * (n_rows0 + 1);
   double* __restrict__ pb = prows + (size_t)b * n_prows * T::K2;
-  // record components: lane l holds int (l & 15) of the chunk's 4 records (i, j, k, w) and the
-  // others read it with a lane shuffle: no register array is indexed at run time
-  const int ucomp = s == 0 ? 1 : 0, vcomp = s == 2 ? 1 : 2;
+  double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * K;
   // staged pieces of one chunk: piece pc = 64 t + lane is SW doubles of row8 = pc / (KP / SW)
-  // (rows 0-3: th_u of obs 0-3, rows 4-7: th_v), columns SW (pc % (KP / SW)) ..
+  // (rows 0-3: th_u = th_j of obs 0-3, rows 4-7: th_v = th_k), columns SW (pc % (KP / SW)) ..
   typedef double d2v __attribute__((ext_vector_type(2)));  // a native vector: SROA-friendly
   using SV = typename std::conditional<T::SW == 2, d2v, double>::type;
   constexpr int PR = T::KP / T::SW;  // pieces per image row
@@ -465,7 +450,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     for (int t = 0; t < T::NPC; ++t) {
       const int pc = 64 * t + lane;
       const int row8 = pc < 8 * PR ? pc / PR : 0, col = T::SW * (pc % PR);
-      const int g = __shfl(rv, (row8 & 3) * 4 + ((row8 >> 2) ? vcomp : ucomp), 64);
+      const int g = __shfl(rv, (row8 & 3) * 4 + ((row8 >> 2) ? 2 : 1), 64);
       v[t] = *reinterpret_cast<const SV*>(th + (size_t)g * K + (col < K ? col : K - T::SW));
     }
   };
@@ -480,22 +465,19 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 #pragma unroll
   for (int t = 0; t < NX16 * NX16; ++t) m16[t] = d4v{0.0, 0.0, 0.0, 0.0};
   double ll = 0.0;
-  // the image's pad columns are read (times a zero Z entry) by the d dot product: keep them 0
+  // the image's pad columns are read (times a zero Z entry) by the d dot product and are the Z'
+  // operand's k >= K rows: keep them 0
   for (int idx = lane; idx < 2 * T::IMG; idx += 64) img[idx] = 0.0;
   wave_lds_sync();
 
-  // w of observation hi (count on stream 0, c index on streams 1 / 2) of a record register
-  auto rec_w = [&](int r) { return __shfl(r, hi * 4 + 3, 64); };
+  // w of observation hi (its count n_r) of a record register
+  auto rec_w = [&](int rr) { return __shfl(rr, hi * 4 + 3, 64); };
   if (any) {
-    // Software pipeline: records U - 1 chunks ahead, theta values (and c) DT ahead; the LDS
-    // image of chunk q + 1 is written at the end of chunk q (double buffer).
+    // Software pipeline: records U - 1 chunks ahead, theta values DT ahead; the LDS image of
+    // chunk q + 1 is written at the end of chunk q (double buffer).
     SV st[U][T::NPC];  // theta values of chunk q in slot (q - c0) % U
-    double cr[U];      // PASS_B: c of observation hi, same slots
 #pragma unroll
-    for (int i = 0; i < DT; ++i) {
-      stage_load(rv[i], st[i]);
-      if constexpr (MODE == PASS_B) cr[i] = cb[rec_w(rv[i])];
-    }
+    for (int i = 0; i < DT; ++i) stage_load(rv[i], st[i]);
     stage_store(img, st[0]);
     for (int q0 = c0; q0 < c1; q0 += U) {
 #pragma unroll
@@ -503,42 +485,59 @@ __global__ __launch_bounds__(NT) void pass_kernel(
         const int q = q0 + ph;
         if (q >= c1) break;
         const int buf = ph & 1;  // U is even: the image buffer alternates with q
-        // prefetch: records of chunk q + U - 1 into the slot chunk q - 1 used, theta / c of q + DT
+        // prefetch: records of chunk q + U - 1 into the slot chunk q - 1 used, theta of q + DT
         rv[(ph + U - 1) % U] = ld_rec(clampq(q + U - 1));
         stage_load(rv[(ph + DT) % U], st[(ph + DT) % U]);
-        if constexpr (MODE == PASS_B) cr[(ph + DT) % U] = cb[rec_w(rv[(ph + DT) % U])];
         wave_lds_sync();
         const double* I = img + buf * T::IMG;
         const int rq = rv[ph % U];
         const int pr0 = __builtin_amdgcn_readlane(rq, 16);
         const int pr1 = __builtin_amdgcn_readlane(rv[(ph + 1) % U], 16);
 
-        double c = MODE == PASS_B ? cr[ph] : 0.0;
-        if constexpr (MODE != PASS_B) {
-          // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
-          const int nw = rec_w(rq);
-          const double* __restrict__ V = Vt + __builtin_amdgcn_readlane(rq, 17) * T::VDBL;
-          double az[NG];  // th_v[obs lo][4 hs + hi]: the A operand of every b group
+        // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
+        const int nw = rec_w(rq);
+        const double* __restrict__ V = Vt + __builtin_amdgcn_readlane(rq, 17) * T::VDBL;
+        double az[NG];  // th_v[obs lo][4 hs + hi]: the A operand of every b group
 #pragma unroll
-          for (int hs = 0; hs < NG; ++hs) az[hs] = I[(4 + lo) * TR + 4 * hs + hi];
-          double dp = 0.0;
+        for (int hs = 0; hs < NG; ++hs) az[hs] = I[(4 + lo) * TR + 4 * hs + hi];
+        double zb[T::NBG];
+        double dp = 0.0;
+#pragma unroll
+        for (int bg = 0; bg < T::NBG; ++bg) {
+          double z = 0.0;
+#pragma unroll
+          for (int hs = 0; hs < NG; ++hs)
+            z = mfma4(az[hs], V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
+          zb[bg] = z;
+          dp = fma(I[hi * TR + 16 * bg + 4 * blk + lo], z, dp);
+        }
+        const double d = row16_sum(dp) + eps;
+        if constexpr (MODE == PASS_LL) {
+          if ((lane & 15) == 0) ll += (double)nw * log(d);
+        } else {
+          const double c = (double)nw / d;
+          // ---- the j- and k-slot sums of this observation (:1009-1011): Y[entry j][b] = c Z[b]
+          // and Y[entry k][h] = c Z'[h], Z'[h] = sum_b th_j[b] V[b][h]; 16 lanes of row hi write
+          // 16 consecutive words of observation hi's entry
+          const int e1 = __shfl(rq, 18 + 2 * hi, 64), e2 = __shfl(rq, 19 + 2 * hi, 64);
+          double au[NG];  // th_u[obs lo][4 bs + hi]: the A operand of Z'
+#pragma unroll
+          for (int bs = 0; bs < NG; ++bs) au[bs] = I[lo * TR + 4 * bs + hi];
 #pragma unroll
           for (int bg = 0; bg < T::NBG; ++bg) {
-            double z = 0.0;
+            const int bb = 16 * bg + 4 * blk + lo;
+            if (bb < K) yb[(size_t)e1 * K + bb] = c * zb[bg];
+          }
 #pragma unroll
-            for (int hs = 0; hs < NG; ++hs)
-              z = mfma4(az[hs], V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
-            dp = fma(I[hi * TR + 16 * bg + 4 * blk + lo], z, dp);
+          for (int hg = 0; hg < T::NBG; ++hg) {
+            double z2 = 0.0;
+            // (columns h >= K of V are zero, past KP the next row's words: finite, never stored)
+#pragma unroll
+            for (int bs = 0; bs < NG; ++bs)
+              z2 = mfma4(au[bs], V[(4 * bs + hi) * VR + 16 * hg + 4 * blk + lo], z2);
+            const int hh = 16 * hg + 4 * blk + lo;
+            if (hh < K) yb[(size_t)e2 * K + hh] = c * z2;
           }
-          const double d = row16_sum(dp) + eps;
-          if constexpr (MODE == PASS_LL) {
-            if ((lane & 15) == 0) ll += (double)nw * log(d);
-          } else {
-            c = (double)nw / d;
-            st_wt(cb + (size_t)q * CH + hi, c);  // the 16 lanes of row hi store the same value
-          }
-        }
-        if constexpr (MODE != PASS_LL) {
           // ---- M += c th_u (x) th_v over the chunk's 4 observations: one v_mfma_f64_16x16x4 per
           // 16 x 16 tile of M, k = the 4 observations.  Lane l holds A[x = l & 15][o = l >> 4] =
           // th_u(obs hi)[x] and B[o = l >> 4][y = l & 15] = c_hi th_v(obs hi)[y]: both come from
@@ -582,7 +581,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   }
   st_.mark(2);
   st_.t[5] = (unsigned long long)(c1 - c0);
-  if constexpr (MODE != PASS_B) st_.t[4] = (unsigned long long)(wg_gene[w + 1] - wg_gene[w]);
+  st_.t[4] = (unsigned long long)(wg_gene[w + 1] - wg_gene[w]);
   if constexpr (MODE == PASS_LL) {
     // fixed-order workgroup sum of the log-likelihood terms
     __shared__ double red[NW];
@@ -597,109 +596,62 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     }
   }
   st_.mark(3);
-  st_.flush(MODE == PASS_B ? 1 : MODE == PASS_A ? 0 : 4, wave_id, lane);
+  st_.flush(MODE == PASS_A ? 0 : 4, wave_id, lane);
 }
 
 // ------------------------------------------------------------------------------------------
-// fin_kernel, grid (gene workgroups + cell workgroups, B), block 256 = 4 waves.
-//   gene part (4 genes = one MFMA row tile per workgroup): for every (stream s, rating r) the
-//     genes' partial rows are summed into LDS (fixed order), then
-//       X[g][x] += sum_k M_{s,r,g}[k] P^s_r[k][x]   (k = the two other axes, dense)
-//     on FP64 MFMA: blocks = x tiles, wave w takes the (combo, x group) items w, w + 4, ...; the
-//     four waves' partial X are summed in LDS in wave order.  theta' = theta X / deg (SUMS: nth).
-//     p is read from the snapshot pold (the cell part below rewrites pr in the same launch).
-//   cell part: S_r = sum of the rating's S partials (fixed order); npr = p S;
-//     p' = npr / (eps + sum_r npr)  (SUMS: S_out = S, p untouched).
+// gene_kernel (the M-step's gene side, launch 2 of an iteration), grid (gene workgroups + S
+// workgroups + Y workgroups, B), block 512:
+//   gene workgroups, 16 genes each (4 MFMA row tiles): for every rating r, the genes' stream-0
+//     partial rows summed into LDS (fixed order), then
+//       X0[g][a] += sum_k M_{r,g}[k] p_r[a][k]    (k = the (b, h) cells, dense)
+//     on FP64 MFMA; wave w takes a group w % NXG and k part w / NXG of all four tiles, so each p
+//     load (from L2) feeds 4 MFMAs; the k parts are added in order.  -> x0[B][P][K]
+//   S workgroups: S_r[a][cell] = sum_q th_g(q)[a] M_q[cell] over ~16 stream-0 partial rows
+//     (s_partial above) -> spart[B][n_sp][K^3]
+//   Y workgroups: thread (g, x) sums gene g's Y entries (contiguous, entry order) -> ysum[B][P][K]
+// Nothing here writes theta or p (upd_kernel does, one launch later), so the S workgroups read
+// the theta the pass used.
 // ------------------------------------------------------------------------------------------
 struct SpRange {
   int lo[MAX_R], hi[MAX_R];
 };
 
 template <int K>
-#ifndef MMSBM_FIN_PL
-#define MMSBM_FIN_PL 0  // 1: big fin with the combo's P^s in LDS where it fits (measured slower:
-                        // K=20 x 8 fin 266 vs 214 us, one workgroup per CU instead of two)
-#endif
 struct FT {
   static constexpr int K2 = K * K, NG = (K + 3) / 4, KP = 4 * NG;
-  static constexpr int KS = (K2 + 3) / 4;       // k-steps over the dense (y, z) cells
+  static constexpr int KS = (K2 + 3) / 4;       // k-steps over the dense (b, h) cells
   static constexpr int K2P = 4 * KS;
-  static constexpr int NXG = (NG + 3) / 4;      // MFMA groups of 4 x tiles
-  // K <= 12: 4 genes per workgroup of 4 waves, p of every rating staged in LDS.  K > 12: 16 genes
-  // (4 MFMA row tiles sharing each p load) per workgroup of 8 waves, one combo at a time in LDS.
-  static constexpr int GT = K <= 12 ? 1 : 4;
-  static constexpr int NGW = 4 * GT;
-  static constexpr int NT = GT == 1 ? 256 : 512;
-  static constexpr int NPART = NT / 64;         // cell part: threads per cell
-  static constexpr int KSPLIT = GT == 1 ? 1 : 8 / NXG;  // big: k-step parts over the 8 waves
-  static constexpr int CB_RAW = (60 * 1024) / (4 * K2P * 8);
-  static constexpr int CB = GT > 1 ? 1 : (CB_RAW > 6 ? 6 : (CB_RAW < 1 ? 1 : CB_RAW));
-  static constexpr int MS_G = GT > 1 ? NGW * K2P + KSPLIT * NGW * KP
-                                     : (CB * 4 * K2P > 4 * NXG * 64 ? CB * 4 * K2P : 4 * NXG * 64);
-  static constexpr int MS = MS_G > MAX_R * NPART * 64 ? MS_G : MAX_R * NPART * 64;  // doubles
-  static constexpr bool PLDS = K <= 12;  // p of every rating staged in LDS (else read from L2)
-  // big fin (K > 12): the combo's P^s staged in LDS as [k][x] (x stride PLK) when it fits beside
-  // the gene rows (K <= 21), instead of each wave reading its p operands from L2
-  static constexpr int PLK = 4 * NG;
-  static constexpr int PLN = K2P * PLK;
-  static constexpr bool PLB = MMSBM_FIN_PL && GT > 1 && (MS + PLN) * 8 <= 160 * 1024;
-  // cell part: CL rounds of 64 cells per workgroup (CL = 8 at K = 20 x 8 samples measured slower:
-  // fin 221 -> 244 us, the longer cell workgroups finish last)
-  static constexpr int CL = 1;
-  static constexpr int NCW = (K * K * K + 64 * CL - 1) / (64 * CL);
-  static constexpr int LDS = (MS + (PLDS ? MAX_R * K * K * K : 0) + (PLB ? PLN : 0)) * 8;
-  // big fin whose LDS lets two workgroups share a CU (K = 20-23): rounds of 6 partial-row entries
-  // and a 128-VGPR budget (4 waves per SIMD; no spills there, K = 14-19 would spill 8-23); above,
-  // LDS allows one workgroup and 12 entries per round keep more loads in flight
-  static constexpr bool TWO = GT > 1 && 2 * LDS <= 160 * 1024 && K >= 20;
-  static constexpr int RE_CAP = (TWO || PLB) ? 6 : 12;  // (PLB: the staged P^s loads are live beside the round)
+  static constexpr int NXG = (NG + 3) / 4;      // MFMA groups of 4 a tiles
+  static constexpr int GT = 4;                  // gene row tiles per workgroup
+  static constexpr int NGW = 4 * GT;            // genes per workgroup
+  static constexpr int NT = 512;
+  static constexpr int KSPLIT = 8 / NXG;        // k-step parts over the 8 waves
+  static constexpr int MS = NGW * K2P + KSPLIT * NGW * KP;  // doubles: summed rows + X parts
+  static constexpr int LDS_SP = 64 * KP;                    // s_partial's theta staging
+  static constexpr int LDS = (MS > LDS_SP ? MS : LDS_SP) * 8;
+  // LDS that lets two workgroups share a CU (K = 20-23): rounds of 6 partial-row entries and a
+  // 128-VGPR budget (4 waves per SIMD); above, LDS allows one workgroup and 12 entries per round
+  // keep more loads in flight (profiles/r02d_fin20_ab.txt: 221 -> 216 us at K = 20 x 8)
+  static constexpr bool TWO = 2 * LDS <= 160 * 1024 && K >= 20;
+  static constexpr int RE_CAP = TWO ? 6 : 12;
   static constexpr int WPE = TWO ? 4 : 1;
-  static_assert(GT == 1 || NXG * KSPLIT == 8, "big fin: one (x group, k part) per wave");
-  static_assert(GT == 1 || NGW * K <= NT, "big fin epilogue: one (gene, x) per thread");
-  static_assert(LDS <= 160 * 1024, "fin LDS over budget");
+  static constexpr int YU = 8;                  // Y entries in flight per thread
+  static_assert(NXG * KSPLIT == 8, "gene part: one (a group, k part) per wave");
+  static_assert(NGW * K <= NT, "gene part epilogue: one (gene, a) per thread");
+  static_assert(LDS <= 160 * 1024, "gene kernel LDS over budget");
 };
 
-// One (combo, x group) item of the fin gene part: sum_k M_g[k] P^s[k][x] over the dense (y, z)
-// cells k on MFMA (k = 4 ks + hi).  P^s[k][x]: s = 0 p[x][y][z] = p[x K2 + k], s = 1 p[y][x][z]
-// (k = y K + z), s = 2 p[y][z][x] = p[k K + x].  Addresses are clamped (k >= K2: M is zero there;
-// x >= K: the column is never stored), so every load is unconditional and a round's loads go out
-// together.
-template <int K, int S>
-__device__ __forceinline__ double x_item(const double* __restrict__ Mg, const double* __restrict__ p,
-                                         int x, int hi) {
-  using F = FT<K>;
-  constexpr int K2 = K * K, UB = F::PLDS ? 8 : 16;
-  const int xc = x < K ? x : K - 1;
-  double a2 = 0.0;
-#pragma unroll 1
-  for (int ks0 = 0; ks0 < F::KS; ks0 += UB) {
-    double av[UB], bv[UB];
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int ks = ks0 + u < F::KS ? ks0 + u : F::KS - 1;
-      const int k = 4 * ks + hi, kc = k < K2 ? k : K2 - 1;
-      int idx;
-      if constexpr (S == 0) idx = xc * K2 + kc;
-      else if constexpr (S == 2) idx = kc * K + xc;
-      else idx = kc + (kc / K) * (K2 - K) + xc * K;
-      const double m = Mg[k];
-      av[u] = ks0 + u < F::KS ? m : 0.0;
-      bv[u] = p[idx];
-    }
-#pragma unroll
-    for (int u = 0; u < UB; ++u) a2 = mfma4(av[u], bv[u], a2);
-  }
-  return a2;
-}
-
-// The same contraction for GT gene tiles at once (big fin): each p load feeds GT MFMAs, over the
-// k-steps [kb, ke).  Mg = tile 0's row of lane lo; tile t's row is Mg + 4 t K2P.
-template <int K, int S>
-__device__ __forceinline__ void x_tiles(const double* __restrict__ Mg, const double* __restrict__ p,
-                                        int x, int hi, int kb, int ke, double (&acc)[FT<K>::GT]) {
+// X0 contraction of GT gene tiles at once: each p load feeds GT MFMAs, over the k-steps [kb, ke).
+// Mg = tile 0's row of lane lo; tile t's row is Mg + 4 t K2P.  p[a][k] = p_r[a K2 + k]; addresses
+// clamped (k >= K2: M is zero there; a >= K: the column is never stored), so every load is
+// unconditional and a round's loads go out together.
+template <int K>
+__device__ __forceinline__ void x0_tiles(const double* __restrict__ Mg, const double* __restrict__ p,
+                                         int a, int hi, int kb, int ke, double (&acc)[FT<K>::GT]) {
   using F = FT<K>;
   constexpr int K2 = K * K, UB = 8, GT = F::GT;
-  const int xc = x < K ? x : K - 1;
+  const int ac = a < K ? a : K - 1;
 #pragma unroll 1
   for (int ks0 = kb; ks0 < ke; ks0 += UB) {
     double bv[UB];
@@ -708,11 +660,7 @@ __device__ __forceinline__ void x_tiles(const double* __restrict__ Mg, const dou
     for (int u = 0; u < UB; ++u) {
       const int ks = ks0 + u < ke ? ks0 + u : ke - 1;
       const int k = 4 * ks + hi, kc = k < K2 ? k : K2 - 1;
-      int idx;
-      if constexpr (S == 0) idx = xc * K2 + kc;
-      else if constexpr (S == 2) idx = kc * K + xc;
-      else idx = kc + (kc / K) * (K2 - K) + xc * K;
-      bv[u] = p[idx];
+      bv[u] = p[ac * K2 + kc];
       kk[u] = k;
     }
 #pragma unroll
@@ -727,46 +675,14 @@ __device__ __forceinline__ void x_tiles(const double* __restrict__ Mg, const dou
   }
 }
 
-// x_tiles with the combo's P^s staged in LDS (FT::PLB): PL[k PLK + x], zero past K^2 and K.
+// Gene part: 16 genes per workgroup (4 MFMA row tiles), 8 waves.  For each rating in order, the
+// 16 genes' stream-0 partial rows are summed into LDS; wave w then takes a group w % NXG and k-step
+// part w / NXG of all 4 gene tiles.  The k parts are added in order in the epilogue.
 template <int K>
-__device__ __forceinline__ void x_tiles_pl(const double* __restrict__ Mg, const double* __restrict__ PL,
-                                           int x, int hi, int kb, int ke, double (&acc)[FT<K>::GT]) {
-  using F = FT<K>;
-  constexpr int UB = 8, GT = F::GT;
-  const int xc = x < K ? x : K - 1;
-#pragma unroll 1
-  for (int ks0 = kb; ks0 < ke; ks0 += UB) {
-    double bv[UB];
-    int kk[UB];
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int ks = ks0 + u < ke ? ks0 + u : ke - 1;
-      const int k = 4 * ks + hi;
-      bv[u] = PL[k * F::PLK + xc];
-      kk[u] = k;
-    }
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const bool ok = ks0 + u < ke;
-#pragma unroll
-      for (int t = 0; t < GT; ++t) {
-        const double m = Mg[t * 4 * F::K2P + kk[u]];
-        acc[t] = mfma4(ok ? m : 0.0, bv[u], acc[t]);
-      }
-    }
-  }
-}
-
-// Gene part of fin_kernel for K > 12: 16 genes per workgroup (4 MFMA row tiles), 8 waves.  For
-// each combo (s, r) in order, the 16 genes' partial rows are summed into LDS; wave w then takes
-// x group w % NXG and k-step part w / NXG of all 4 gene tiles, so each p load feeds 4 MFMAs.
-// The k parts are added in order in the epilogue.
-template <int K, bool SUMS>
-__device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const double* __restrict__ pold,
-                                              const double* __restrict__ prows,
-                                              const int* __restrict__ prow_ptr, const int* __restrict__ deg,
-                                              int P, int R, long long n_prows, double* __restrict__ nth_out,
-                                              const double* __restrict__ nth_add, double* Ms, Stamp& st_) {
+__device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const double* __restrict__ prows,
+                                         const int* __restrict__ prow_ptr, int P, int R,
+                                         long long n_prows, double* __restrict__ x0, double* Ms,
+                                         Stamp& st_) {
   using F = FT<K>;
   constexpr int K2 = F::K2, K3 = K * K * K, NGW = F::NGW, NT = F::NT, KP = F::KP;
   const int tid = threadIdx.x, b = blockIdx.y;
@@ -774,55 +690,48 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
   const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
   const int g0 = blockIdx.x * NGW;
   const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
-  const int NC = 3 * R;
   double* Xr = Ms + NGW * F::K2P;  // [KSPLIT][NGW][KP]
-  // epilogue operands (thread t < NGW K: gene g0 + t / K, x = t % K), loaded up front
-  const int eg = tid / K, ex = tid % K;
-  const int ge = g0 + eg < P ? g0 + eg : P - 1;
-  const double th_e = theta[((size_t)b * P + ge) * K + ex];
-  const double ad_e = nth_add ? nth_add[((size_t)b * P + ge) * K + ex] : 0.0;
-  const int deg_e = deg[ge];
-  __shared__ int pp[3 * MAX_R][NGW + 1];
+  __shared__ int pp[MAX_R][NGW + 1];
   {
     const int c = tid / (NGW + 1), i = tid % (NGW + 1);
-    const int v = prow_ptr[(size_t)(c < NC ? c : 0) * (P + 1) + (g0 + i < P ? g0 + i : P)];
-    if (c < NC) pp[c][i] = v;
+    const int v = prow_ptr[(size_t)(c < R ? c : 0) * (P + 1) + (g0 + i < P ? g0 + i : P)];
+    if (c < R) pp[c][i] = v;
   }
   const int xg = wv % F::NXG, ksp = wv / F::NXG;
   const int kb = F::KS * ksp / F::KSPLIT, ke = F::KS * (ksp + 1) / F::KSPLIT;
-  const int x = 4 * (4 * xg + blk) + lo;
+  const int a = 4 * (4 * xg + blk) + lo;
   double acc[F::GT];
 #pragma unroll
   for (int t = 0; t < F::GT; ++t) acc[t] = 0.0;
   constexpr int NE = NGW * F::K2P;
   constexpr int NEPT = (NE + NT - 1) / NT, RE = NEPT < F::RE_CAP ? NEPT : F::RE_CAP;
   // one round of RE entries per thread: each entry's first two partial rows loaded with the whole
-  // round in flight (addresses clamped, loads unconditional); the first round of the next combo
-  // is loaded before this combo's contraction, so its latency hides under the MFMAs.  Only the
+  // round in flight (addresses clamped, loads unconditional); the first round of the next rating
+  // is loaded before this rating's contraction, so its latency hides under the MFMAs.  Only the
   // loaded values stay live; ranges are re-read from LDS when the round is stored.
   double v1[RE], v2[RE];
-  auto entry = [&](int combo, int idx, int& qa, int& qb, int& kk) {
+  auto entry = [&](int r, int idx, int& qa, int& qb, int& kk) {
     const int gl = idx / F::K2P, k = idx % F::K2P;
     const bool ok = idx < NE && k < K2;
-    qa = ok ? pp[combo][gl] : 0;
-    qb = ok ? pp[combo][gl + 1] : 0;
+    qa = ok ? pp[r][gl] : 0;
+    qb = ok ? pp[r][gl + 1] : 0;
     kk = k < K2 ? k : 0;
   };
-  auto load_round = [&](int combo, int i0) {
+  auto load_round = [&](int r, int i0) {
 #pragma unroll
     for (int u = 0; u < RE; ++u) {
       int qa, qb, kk;
-      entry(combo, i0 + u * NT, qa, qb, kk);
+      entry(r, i0 + u * NT, qa, qb, kk);
       v1[u] = pb[(size_t)(qa < qb ? qa : 0) * K2 + kk];
       v2[u] = pb[(size_t)(qa + 1 < qb ? qa + 1 : 0) * K2 + kk];
     }
   };
-  auto store_round = [&](int combo, int i0) {
+  auto store_round = [&](int r, int i0) {
 #pragma unroll
     for (int u = 0; u < RE; ++u) {
       const int idx = i0 + u * NT;
       int qa, qb, kk;
-      entry(combo, idx, qa, qb, kk);
+      entry(r, idx, qa, qb, kk);
       double m = qa < qb ? v1[u] : 0.0;
       if (qa + 1 < qb) m += v2[u];
       for (int q = qa + 2; q < qb; ++q) m += pb[(size_t)q * K2 + kk];
@@ -830,260 +739,137 @@ __device__ __forceinline__ void fin_genes_big(double* __restrict__ theta, const 
     }
   };
   __syncthreads();  // pp
-  load_round(0, tid);
-  double* PL = Ms + F::MS;  // FT::PLB: the combo's P^s[k][x]
-  constexpr int NPL = (F::PLN + NT - 1) / NT;
-  for (int combo = 0; combo < NC; ++combo) {
-    __syncthreads();  // the previous combo's contraction is done with Ms
+  // ratings whose 16 genes have no stream-0 partial row contribute zero: skipped (uniform)
+  auto live = [&](int r) { return pp[r][0] < pp[r][NGW]; };
+  int rn = 0;
+  while (rn < R && !live(rn)) ++rn;
+  if (rn < R) load_round(rn, tid);
+  for (int r = rn; r < R;) {
+    int nxt = r + 1;
+    while (nxt < R && !live(nxt)) ++nxt;
+    __syncthreads();  // the previous rating's contraction is done with Ms
     st_.mark(4);
-    if constexpr (F::PLB) {  // stage P^s of this combo: loads out first, stored after the rows
-      const int s = combo / R, r = combo % R;
-      const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
-      double pl[NPL];
-#pragma unroll
-      for (int i = 0; i < NPL; ++i) {
-        const int e = tid + NT * i, k = e / F::PLK, xx = e % F::PLK;
-        const bool ok = e < F::PLN && k < K2 && xx < K;
-        const int kc = ok ? k : 0, xc = ok ? xx : 0;
-        const int idx = s == 0 ? xc * K2 + kc : s == 2 ? kc * K + xc : kc + (kc / K) * (K2 - K) + xc * K;
-        const double v = p[idx];
-        pl[i] = ok ? v : 0.0;
-      }
-      store_round(combo, tid);
-#pragma unroll
-      for (int i = 0; i < NPL; ++i)
-        if (tid + NT * i < F::PLN) PL[tid + NT * i] = pl[i];
-    } else {
-      store_round(combo, tid);
-    }
+    store_round(r, tid);
     for (int i0 = tid + RE * NT; i0 < NE; i0 += RE * NT) {
-      load_round(combo, i0);
-      store_round(combo, i0);
+      load_round(r, i0);
+      store_round(r, i0);
     }
     st_.mark(5);
     __syncthreads();
     st_.mark(1);
-    if (combo + 1 < NC) load_round(combo + 1, tid);
-    const int s = combo / R, r = combo % R;
-    const double* __restrict__ p = pold + ((size_t)b * R + r) * K3;
-    const double* __restrict__ Mg = Ms + (size_t)lo * F::K2P;
-    if constexpr (F::PLB) x_tiles_pl<K>(Mg, PL, x, hi, kb, ke, acc);
-    else if (s == 0) x_tiles<K, 0>(Mg, p, x, hi, kb, ke, acc);
-    else if (s == 1) x_tiles<K, 1>(Mg, p, x, hi, kb, ke, acc);
-    else x_tiles<K, 2>(Mg, p, x, hi, kb, ke, acc);
+    if (nxt < R) load_round(nxt, tid);
+    const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
+    x0_tiles<K>(Ms + (size_t)lo * F::K2P, p, a, hi, kb, ke, acc);
+    r = nxt;
   }
   st_.mark(2);
-  // X[gene 4 t + hi][x]: the k parts added in order
+  // X0[gene 4 t + hi][a]: the k parts added in order
 #pragma unroll
   for (int t = 0; t < F::GT; ++t)
-    if (x < K) Xr[(ksp * NGW + 4 * t + hi) * KP + x] = acc[t];
+    if (a < K) Xr[(ksp * NGW + 4 * t + hi) * KP + a] = acc[t];
   __syncthreads();
+  const int eg = tid / K, ex = tid % K;
   if (tid < NGW * K && g0 + eg < P) {
     double X = Xr[eg * KP + ex];
 #pragma unroll
     for (int q = 1; q < F::KSPLIT; ++q) X += Xr[(q * NGW + eg) * KP + ex];
-    if (nth_add) X += ad_e;
-    const size_t o = ((size_t)b * P + g0 + eg) * K + ex;
-    if constexpr (SUMS) nth_out[o] = X;
-    else theta[o] = th_e * X / (double)deg_e;
+    x0[((size_t)b * P + g0 + eg) * K + ex] = X;
   }
   st_.mark(3);
   st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 8 + wv, lane);
 }
 
-template <int K, bool SUMS>
-__global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>::WPE))) void fin_kernel(
-    double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ pold,
-    const double* __restrict__ prows, const int* __restrict__ prow_ptr,
-    const double* __restrict__ spart, const int* __restrict__ deg, SpRange spr, int P, int R,
-    long long n_prows, int n_sp, int n_gene_wg, double eps, double* __restrict__ nth_out,
-    double* __restrict__ S_out, const double* __restrict__ nth_add,
-    const double* __restrict__ q_part, double* __restrict__ q_out, int n_qwg) {
-  using F = FT<K>;
-  constexpr int K2 = F::K2, K3 = K * K * K, NG = F::NG;
-  extern __shared__ __attribute__((aligned(16))) double Ms[];  // [CB][4 genes][K2P]
-  const int tid = threadIdx.x, b = blockIdx.y;
+// Y part: thread (g, x) = item sums component x of gene g's Y entries [yptr[g], yptr[g + 1]) in
+// entry order, YU loads in flight (a hub gene has many entries).
+template <int K>
+__device__ __forceinline__ void genes_ysum(const double* __restrict__ yb, const int* __restrict__ yptr,
+                                           long long item, int P, double* __restrict__ ysum_b) {
+  constexpr int YU = FT<K>::YU;
+  if (item >= (long long)P * K) return;
+  const int g = (int)(item / K), x = (int)(item % K);
+  const int e0 = yptr[g], e1 = yptr[g + 1];
+  double S = 0.0;
+  for (int e = e0; e < e1; e += YU) {
+    double v[YU];
+#pragma unroll
+    for (int u = 0; u < YU; ++u) v[u] = yb[(size_t)(e + u < e1 ? e + u : e) * K + x];
+#pragma unroll
+    for (int u = 0; u < YU; ++u)
+      if (e + u < e1) S += v[u];
+  }
+  ysum_b[item] = S;
+}
+
+template <int K>
+__global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>::WPE))) void gene_kernel(
+    const double* __restrict__ theta, const double* __restrict__ pr, const double* __restrict__ prows,
+    const int* __restrict__ prow_ptr, const int* __restrict__ prow_gene, const int* __restrict__ sp_desc,
+    const double* __restrict__ ybuf, const int* __restrict__ yptr, double* __restrict__ x0,
+    double* __restrict__ ysum, double* __restrict__ spart, int P, int R, long long n_prows,
+    long long n_y, int n_sp, int n_gene_wg, int n_sp_wg) {
+  using T = KT<K>;
+  extern __shared__ __attribute__((aligned(16))) double Ms[];
+  const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
   Stamp st_{};
   st_.mark(0);
-  if constexpr (F::GT > 1) {
-    if ((int)blockIdx.x < n_gene_wg) {
-      fin_genes_big<K, SUMS>(theta, pold, prows, prow_ptr, deg, P, R, n_prows, nth_out, nth_add, Ms, st_);
-      return;
-    }
-  }
-  if (F::GT == 1 && (int)blockIdx.x < n_gene_wg) {
-    const int lane = tid & 63, wv = tid >> 6;
+  if (w < n_gene_wg) {
+    genes_x0<K>(pr, prows, prow_ptr, P, R, n_prows, x0, Ms, st_);
+  } else if (w < n_gene_wg + n_sp_wg) {
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
-    const int g0 = blockIdx.x * 4;
-    const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
-    const int NC = 3 * R;
-    double* Ps = Ms + F::MS;  // [R][K3] when F::PLDS
-    // epilogue operands (wave 0: gene g0 + hi, x = 4 (4 xg + blk) + lo), loaded up front
-    const int ge = g0 + hi < P ? g0 + hi : P - 1;
-    double th_e[F::NXG], ad_e[F::NXG];
-#pragma unroll
-    for (int xg = 0; xg < F::NXG; ++xg) {
-      const int x = 4 * (4 * xg + blk) + lo;
-      th_e[xg] = theta[((size_t)b * P + ge) * K + (x < K ? x : 0)];
-      ad_e[xg] = nth_add ? nth_add[((size_t)b * P + ge) * K + (x < K ? x : 0)] : 0.0;
-    }
-    const int deg_e = deg[ge];
-    // partial-row ranges of the 4 genes for every combo (= s * R + r) and p, staged in LDS with
-    // all their loads in flight together
-    __shared__ int pp[3 * MAX_R][5];
-    {
-      const int c = tid / 5, i = tid % 5;
-      const int v = prow_ptr[(size_t)(c < NC ? c : 0) * (P + 1) + (g0 + i < P ? g0 + i : P)];
-      if constexpr (F::PLDS) {
-        for (int base = 0; base < R * K3; base += 8 * FIN_NT) {
-          double pv[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int idx = base + u * FIN_NT + tid;
-            pv[u] = pold[(size_t)b * R * K3 + (idx < R * K3 ? idx : 0)];
-          }
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            if (base + u * FIN_NT + tid < R * K3) Ps[base + u * FIN_NT + tid] = pv[u];
-        }
-      }
-      if (tid < NC * 5) pp[c][i] = v;
-    }
-    double acc[F::NXG];
-#pragma unroll
-    for (int xg = 0; xg < F::NXG; ++xg) acc[xg] = 0.0;
-    for (int cb0 = 0; cb0 < NC; cb0 += F::CB) {
-      const int ncb = NC - cb0 < F::CB ? NC - cb0 : F::CB;
-      const int NE = ncb * 4 * F::K2P;
-      __syncthreads();
-      st_.mark(4);
-      // Ms[c][gene][k] = the gene's partial rows summed in row order; RE entries per thread per
-      // round (one round for K <= 12), their first two rows loaded together (addresses clamped,
-      // loads unconditional)
-      constexpr int NEPT = (F::CB * 4 * F::K2P + FIN_NT - 1) / FIN_NT, RE = NEPT < 12 ? NEPT : 12;
-      for (int i0 = tid; i0 < NE; i0 += RE * FIN_NT) {
-        int qa[RE], qb[RE], kk[RE];
-        double v1[RE], v2[RE];
-#pragma unroll
-        for (int u = 0; u < RE; ++u) {
-          const int idx = i0 + u * FIN_NT;
-          const int c = idx / (4 * F::K2P), rem = idx % (4 * F::K2P);
-          const int gl = rem / F::K2P, k = rem % F::K2P;
-          const bool ok = idx < NE && k < K2;
-          qa[u] = ok ? pp[cb0 + c][gl] : 0;
-          qb[u] = ok ? pp[cb0 + c][gl + 1] : 0;
-          kk[u] = k < K2 ? k : 0;
-          v1[u] = pb[(size_t)(qa[u] < qb[u] ? qa[u] : 0) * K2 + kk[u]];
-          v2[u] = pb[(size_t)(qa[u] + 1 < qb[u] ? qa[u] + 1 : 0) * K2 + kk[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < RE; ++u) {
-          const int idx = i0 + u * FIN_NT;
-          double m = qa[u] < qb[u] ? v1[u] : 0.0;
-          if (qa[u] + 1 < qb[u]) m += v2[u];
-          for (int q = qa[u] + 2; q < qb[u]; ++q) m += pb[(size_t)q * K2 + kk[u]];
-          if (idx < NE) Ms[idx] = m;
-        }
-        st_.mark(5);
-      }
-      __syncthreads();
-      st_.mark(1);
-      for (int item = wv; item < ncb * F::NXG; item += 4) {
-        const int c = item / F::NXG, xg = item % F::NXG;
-        const int combo = cb0 + c, s = combo / R, r = combo % R;
-        const double* __restrict__ p = (F::PLDS ? Ps : pold + (size_t)b * R * K3) + (size_t)r * K3;
-        const int x = 4 * (4 * xg + blk) + lo;
-        const double* __restrict__ Mg = Ms + ((size_t)c * 4 + lo) * F::K2P;
-        const double a2 = s == 0 ? x_item<K, 0>(Mg, p, x, hi)
-                                 : s == 1 ? x_item<K, 1>(Mg, p, x, hi) : x_item<K, 2>(Mg, p, x, hi);
-#pragma unroll
-        for (int q = 0; q < F::NXG; ++q)
-          if (q == xg) acc[q] += a2;
-      }
-    }
-    // X[gene hi][x = 4 (4 xg + blk) + lo]: the four waves' partials summed in wave order
-    st_.mark(2);
-    __syncthreads();
-#pragma unroll
-    for (int xg = 0; xg < F::NXG; ++xg) Ms[(wv * F::NXG + xg) * 64 + lane] = acc[xg];
-    __syncthreads();
-    if (wv == 0) {
-      const int g = g0 + hi;
-#pragma unroll
-      for (int xg = 0; xg < F::NXG; ++xg) {
-        const int x = 4 * (4 * xg + blk) + lo;
-        double X = 0.0;
-        for (int w = 0; w < 4; ++w) X += Ms[(w * F::NXG + xg) * 64 + lane];
-        if (nth_add) X += ad_e[xg];
-        if (g < P && x < K) {
-          const size_t o = ((size_t)b * P + g) * K + x;
-          if constexpr (SUMS) nth_out[o] = X;
-          else theta[o] = th_e[xg] * X / (double)deg_e;
-        }
-      }
-    }
-    st_.mark(3);
-    st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 4 + wv, lane);
-  } else if ((int)blockIdx.x >= n_gene_wg + F::NCW) {
-    // joint model q cells (include/mmsbm_pairs.h): 64 cells of qr per workgroup, NPART threads
-    // per cell each summing a share of the pair launch's S2 partials [B][n_qwg][R][K2] (16 loads
-    // in flight), the shares combined in order; qr <- qr S2 / (eps + sum_r qr S2) (:1660-1666)
-    constexpr int NPART = F::NPART;
-    const int cl = tid & 63, part = tid >> 6;
-    const int cell = (blockIdx.x - n_gene_wg - F::NCW) * 64 + cl;
-    const bool cv = cell < K2;
-    const int cc = cv ? cell : 0;
-    double qo[MAX_R];
-#pragma unroll
-    for (int r = 0; r < MAX_R; ++r) qo[r] = q_out[((size_t)b * R + (r < R ? r : R - 1)) * K2 + cc];
-    const int s0 = n_qwg * part / NPART, s1 = n_qwg * (part + 1) / NPART;
-    for (int r = 0; r < R; ++r) {
-      double S = 0.0;
-      for (int w = s0; w < s1; w += 16) {
-        double v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const double x = q_part[(((size_t)b * n_qwg + (w + u < s1 ? w + u : s0)) * R + r) * K2 + cc];
-          v[u] = w + u < s1 ? x : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) S += v[u];
-      }
-      Ms[(r * NPART + part) * 64 + cl] = S;
-    }
-    __syncthreads();
-    if (part == 0 && cv) {
-      double nq[MAX_R];
-      double den = eps;
-#pragma unroll
-      for (int r = 0; r < MAX_R; ++r) {
-        if (r < R) {
-          double S = Ms[r * NPART * 64 + cl];
-#pragma unroll
-          for (int q = 1; q < NPART; ++q) S += Ms[(r * NPART + q) * 64 + cl];
-          nq[r] = qo[r] * S;
-          den += nq[r];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < MAX_R; ++r)
-        if (r < R) q_out[((size_t)b * R + r) * K2 + cell] = nq[r] / den;
-    }
+    const int sw = w - n_gene_wg, sp = sw / T::NIG, ig = sw % T::NIG;
+    const int* d = sp_desc + 3 * sp;
+    s_partial<K>(theta + (size_t)b * P * K, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
+                 spart + ((size_t)b * n_sp + sp) * T::K3, Ms, ig, tid, wv, hi, blk, lo, st_);
+    st_.flush(3, ((long long)b * gridDim.x + w) * NW + wv, lane);
   } else {
-    // CL rounds of 64 cells per workgroup, NPART threads per cell, each summing a share of every
-    // rating's S partials (16 loads in flight), the shares combined in order through LDS
-    constexpr int NPART = F::NPART;
-    const int cl = tid & 63, part = tid >> 6;
-    for (int sub = 0; sub < F::CL; ++sub) {
-    const int cb0 = ((blockIdx.x - n_gene_wg) * F::CL + sub) * 64;
-    if (cb0 >= K3) break;  // uniform over the workgroup
-    if (sub > 0) __syncthreads();  // the previous round's reads of Ms are done
-    const int cell = cb0 + cl;
+    const long long item = (long long)(w - n_gene_wg - n_sp_wg) * FT<K>::NT + tid;
+    genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * K, yptr, item, P, ysum + (size_t)b * P * K);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// upd_kernel (launch 3), grid (theta workgroups + cell workgroups + q workgroups, B), block 512:
+//   theta workgroups: thread (g, a): X = x0 + ysum (+ the joint model's pair sums);
+//     theta' = theta X / deg (:1016-1018), or SUMS: nth = X
+//   cell workgroups: 64 cells x 8 parts; S_r = sum of the rating's S partials (fixed order);
+//     p' = p S / (eps + sum_r p S) in place (:1021-1028), or SUMS: S_out = S
+//   q workgroups (joint model, include/mmsbm_pairs.h): qr from the pair launch's S2 partials
+// ------------------------------------------------------------------------------------------
+constexpr int UPD_NT = 512;
+
+template <int K, bool SUMS>
+__global__ __launch_bounds__(UPD_NT) void upd_kernel(
+    double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ x0,
+    const double* __restrict__ ysum, const double* __restrict__ spart, const int* __restrict__ deg,
+    SpRange spr, int P, int R, int n_sp, int n_th_wg, double eps, double* __restrict__ nth_out,
+    double* __restrict__ S_out, const double* __restrict__ nth_add, const double* __restrict__ q_part,
+    double* __restrict__ q_out, int n_qwg) {
+  constexpr int K2 = K * K, K3 = K * K * K;
+  constexpr int NCW = (K3 + 63) / 64, NPART = UPD_NT / 64;
+  __shared__ double red[MAX_R * NPART * 64];
+  const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
+  if (w < n_th_wg) {
+    const long long item = (long long)w * UPD_NT + tid;
+    if (item >= (long long)P * K) return;  // no barrier in this branch
+    const size_t o = (size_t)b * P * K + item;
+    double X = x0[o] + ysum[o];
+    if (nth_add) X += nth_add[o];
+    if constexpr (SUMS) nth_out[o] = X;
+    else theta[o] = theta[o] * X / (double)deg[item / K];
+    return;
+  }
+  const int cl = tid & 63, part = tid >> 6;
+  if (w < n_th_wg + NCW) {
+    // NPART threads per cell, each summing a share of every rating's S partials (16 loads in
+    // flight), the shares combined in order through LDS
+    const int cell = (w - n_th_wg) * 64 + cl;
     const bool cv = cell < K3;
     const int cc = cv ? cell : 0;
     double po[MAX_R];
 #pragma unroll
-    for (int r = 0; r < MAX_R; ++r) po[r] = pold[((size_t)b * R + (r < R ? r : R - 1)) * K3 + cc];
+    for (int r = 0; r < MAX_R; ++r) po[r] = pr[((size_t)b * R + (r < R ? r : R - 1)) * K3 + cc];
     for (int r = 0; r < R; ++r) {
       const int n = spr.hi[r] - spr.lo[r];
       const int s0 = spr.lo[r] + n * part / NPART, s1 = spr.lo[r] + n * (part + 1) / NPART;
@@ -1098,7 +884,7 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
 #pragma unroll
         for (int u = 0; u < 16; ++u) S += v[u];
       }
-      Ms[(r * NPART + part) * 64 + cl] = S;
+      red[(r * NPART + part) * 64 + cl] = S;
     }
     __syncthreads();
     if (part == 0 && cv) {
@@ -1107,9 +893,9 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
 #pragma unroll
       for (int r = 0; r < MAX_R; ++r) {
         if (r < R) {
-          double S = Ms[r * NPART * 64 + cl];
+          double S = red[r * NPART * 64 + cl];
 #pragma unroll
-          for (int q = 1; q < NPART; ++q) S += Ms[(r * NPART + q) * 64 + cl];
+          for (int q = 1; q < NPART; ++q) S += red[(r * NPART + q) * 64 + cl];
           if constexpr (SUMS) {
             S_out[((size_t)b * R + r) * K3 + cell] = S;
           } else {
@@ -1124,7 +910,49 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
           if (r < R) pr[((size_t)b * R + r) * K3 + cell] = npr[r] / den;
       }
     }
+    return;
+  }
+  // joint model q cells: 64 cells of qr per workgroup, NPART threads per cell each summing a share
+  // of the pair launch's S2 partials [B][n_qwg][R][K2] (16 loads in flight), the shares combined in
+  // order; qr <- qr S2 / (eps + sum_r qr S2) (src/TrigenicInteractionPredictor_23.py:1660-1666)
+  const int cell = (w - n_th_wg - NCW) * 64 + cl;
+  const bool cv = cell < K2;
+  const int cc = cv ? cell : 0;
+  double qo[MAX_R];
+#pragma unroll
+  for (int r = 0; r < MAX_R; ++r) qo[r] = q_out[((size_t)b * R + (r < R ? r : R - 1)) * K2 + cc];
+  const int s0 = n_qwg * part / NPART, s1 = n_qwg * (part + 1) / NPART;
+  for (int r = 0; r < R; ++r) {
+    double S = 0.0;
+    for (int ww = s0; ww < s1; ww += 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const double x = q_part[(((size_t)b * n_qwg + (ww + u < s1 ? ww + u : s0)) * R + r) * K2 + cc];
+        v[u] = ww + u < s1 ? x : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) S += v[u];
     }
+    red[(r * NPART + part) * 64 + cl] = S;
+  }
+  __syncthreads();
+  if (part == 0 && cv) {
+    double nq[MAX_R];
+    double den = eps;
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) {
+      if (r < R) {
+        double S = red[r * NPART * 64 + cl];
+#pragma unroll
+        for (int q = 1; q < NPART; ++q) S += red[(r * NPART + q) * 64 + cl];
+        nq[r] = qo[r] * S;
+        den += nq[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+      if (r < R) q_out[((size_t)b * R + r) * K2 + cell] = nq[r] / den;
   }
 }
 
@@ -1132,7 +960,7 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
 // M-step from summed accumulators (link-sharded iteration, after the cross-rank all-reduce):
 //   theta[g][a] <- theta[g][a] * nth[g][a] / deg[g]                          (:1016-1018)
 //   p_r <- p_r S_r / (eps + sum_r p_r S_r)                                      (:1021-1028)
-// with the same operation order as fin_kernel.  Grid (ceil((P K + K^3) / 256), B).
+// with the same operation order as upd_kernel.  Grid (ceil((P K + K^3) / 256), B).
 // ------------------------------------------------------------------------------------------
 template <int K>
 __global__ __launch_bounds__(256) void mapply_kernel(double* __restrict__ theta, double* __restrict__ pr,
@@ -1233,6 +1061,8 @@ struct SetDev {  // device copy of one link set's plan
   int* prow_ptr = nullptr;
   int* prow_gene = nullptr;
   int* sp_desc = nullptr;
+  int* row_y = nullptr;                 // large-K EM plans: Y entries of each stream-0 row,
+  int* yptr = nullptr;                  // and each gene's entry range
   int* sku[2] = {nullptr, nullptr};     // small-K plans (sk.h): slot descriptors of each group,
   int4* skr[2] = {nullptr, nullptr};    // slot-major records,
   int* skrow12 = nullptr;               // slot-major row12 of group 0
@@ -1240,7 +1070,7 @@ struct SetDev {  // device copy of one link set's plan
   int unit_target = 0;
   void release() {
     void* ps[] = {rows, chunk_prow, chunk_vslot, wg_units, wg_code, wg_gene, vgenes, prow_ptr, prow_gene, sp_desc,
-                  sku[0], sku[1], skr[0], skr[1], skrow12};
+                  row_y, yptr, sku[0], sku[1], skr[0], skr[1], skrow12};
     for (void* p : ps)
       if (p) (void)hipFree(p);
     *this = SetDev();
@@ -1279,7 +1109,9 @@ struct mmsbm_ctx {
   bool zero_degree = false;
   char* ws = nullptr;
   long long ws_bytes = 0;
-  double *cbuf = nullptr, *prows = nullptr, *spart = nullptr, *pold = nullptr, *partL = nullptr;
+  // workspace views: cbuf = small-K c / large-K Y entries, prows = small-K X / large-K M^0 partial
+  // rows, spart = S partials, gx = large-K x0 then ysum ([2][B][P][K])
+  double *cbuf = nullptr, *prows = nullptr, *spart = nullptr, *gx = nullptr, *partL = nullptr;
   double *nth_tmp = nullptr, *S_tmp = nullptr;  // fin_kernel sums-out scratch (kernel timing)
   const double* nth_add = nullptr;  // joint model: pair sums added before the degree division
   const double* q_part = nullptr;   // joint model: S2 partials for fin's q cells (null = none)
@@ -1306,7 +1138,7 @@ struct mmsbm_ctx {
 namespace {
 
 struct WsLayout {
-  size_t cbuf, prows, spart, pold, partL, nth, S, total;
+  size_t cbuf, prows, spart, gx, partL, nth, S, total;
 };
 
 WsLayout ws_layout(const mmsbm_ctx* c) {
@@ -1324,7 +1156,7 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
     off += align_up(B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
     L.spart = off;
     off += align_up(B * std::max(tr.n_wg_a, 1) * K3 * 8);
-    L.pold = off;
+    L.gx = off;
     L.partL = off;
     off += align_up(B * std::max({tr.n_wg_a, te.n_wg_a, 1}) * 8);
     L.nth = off;
@@ -1334,14 +1166,16 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
     L.total = off;
     return L;
   }
+  // large-K: Y entries (+ the dummy entry of padding rows), M^0 partial rows, S partials, x0 and
+  // ysum, likelihood partials, fin's sums-out scratch
   L.cbuf = off;
-  off += align_up(B * (tr.n_rows0 + 1) * 8);
+  off += align_up(B * (tr.n_y + 1) * c->K * 8);
   L.prows = off;
   off += align_up(B * std::max<long long>(tr.n_prows, 1) * K2 * 8);
   L.spart = off;
   off += align_up(B * std::max(tr.n_sp, 1) * K3 * 8);
-  L.pold = off;
-  off += align_up(B * c->R * K3 * 8);
+  L.gx = off;
+  off += align_up(2 * B * (size_t)c->P * c->K * 8);
   L.partL = off;
   off += align_up(B * std::max({tr.n_wg_a, te.n_wg_a, 1}) * 8);
   L.nth = off;
@@ -1380,66 +1214,64 @@ template <int K>
 int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const double* pr,
                 hipStream_t s) {
   using T = KT<K>;
+  using F = FT<K>;
   const SetDev& sd = c->sets[which];
   const auto& h = sd.h;
-  if (mode == PASS_B) {
-    const int n = h.n_wg_b + h.n_sp * T::NIG;
-    if (n == 0) return MMSBM_OK;
-    pass_kernel<K, PASS_B><<<dim3(n, c->B), NT, T::LDS_B, s>>>(
-        sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.wg_units + (size_t)h.n_wg_a * (NW + 1),
-        sd.wg_code + h.n_wg_a, sd.wg_gene, sd.vgenes, sd.sp_desc, sd.prow_gene, theta, pr, c->cbuf,
-        c->prows, c->spart, c->pold, c->partL, c->P, c->R, h.n_rows0, h.n_prows, h.n_wg_b, h.n_sp,
-        c->eps, c->gcap);
+  int rc;
+  if (mode == PASS_B) {  // launch 2: the gene kernel (x0, S partials, Y sums) of the train plan
+    const int ngw = (c->P + F::NGW - 1) / F::NGW;
+    const int nspw = std::max(h.n_sp, 1) * T::NIG;
+    const int nyw = (int)(((long long)c->P * K + F::NT - 1) / F::NT);
+    if ((rc = lds_opt_in(c, 8, &gene_kernel<K>, F::LDS))) return rc;
+    const size_t pk = (size_t)c->B * c->P * K;
+    gene_kernel<K><<<dim3(ngw + nspw + nyw, c->B), F::NT, F::LDS, s>>>(
+        theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
+        c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, nspw);
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
-    int rc;
     // dynamic LDS for the context's gene cap (<= the compile-time GMAX the opt-in covers)
     const int lds = c->gcap * (T::VDBL + T::KP) * 8 + T::IMG_BYTES + 64;
     if (mode == PASS_A) {
       if ((rc = lds_opt_in(c, 0, &pass_kernel<K, PASS_A>, T::LDS_A))) return rc;
       pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
-          sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
-          sd.sp_desc, sd.prow_gene, theta, pr, c->cbuf, c->prows, c->spart, c->pold, c->partL, c->P,
-          c->R, h.n_rows0, h.n_prows, h.n_wg_a, h.n_sp, c->eps, c->gcap);
+          sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.row_y, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
+          theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, h.n_y, h.n_prows, h.n_wg_a, c->eps, c->gcap);
     } else {
       if ((rc = lds_opt_in(c, 1, &pass_kernel<K, PASS_LL>, T::LDS_A))) return rc;
       pass_kernel<K, PASS_LL><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
-          sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
-          sd.sp_desc, sd.prow_gene, theta, pr, c->cbuf, c->prows, c->spart, c->pold, c->partL, c->P,
-          c->R, h.n_rows0, h.n_prows, h.n_wg_a, h.n_sp, c->eps, c->gcap);
+          sd.rows, sd.chunk_prow, sd.chunk_vslot, nullptr, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
+          theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, 0, h.n_prows, h.n_wg_a, c->eps, c->gcap);
     }
   }
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
 
+// launch 3: upd_kernel (theta from x0 + ysum, p from the S partials; sums-out mode for the
+// link-sharded accumulate and kernel timing)
 template <int K>
 int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, double* S,
                hipStream_t s) {
-  using T = KT<K>;
   const SetDev& sd = c->sets[MMSBM_SET_TRAIN];
   const auto& h = sd.h;
-  const int ngw = (c->P + FT<K>::NGW - 1) / FT<K>::NGW;
-  const int ncw = FT<K>::NCW;
-  int rc;
-  if ((rc = lds_opt_in(c, sums ? 3 : 2, sums ? &fin_kernel<K, true> : &fin_kernel<K, false>, FT<K>::LDS)))
-    return rc;
-  const int lds = (FT<K>::MS + (FT<K>::PLDS ? c->R * T::K3 : 0) + (FT<K>::PLB ? FT<K>::PLN : 0)) * 8;
+  const int nthw = (int)(((long long)c->P * K + UPD_NT - 1) / UPD_NT);
+  const int ncw = (K * K * K + 63) / 64;
   SpRange spr{};
   for (int r = 0; r < c->R; ++r) {
     spr.lo[r] = h.sp_lo[r];
     spr.hi[r] = h.sp_hi[r];
   }
+  const size_t pk = (size_t)c->B * c->P * K;
   // joint model: the q cells (qr M-step from the pair launch's S2 partials), theta update only
   const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
   if (sums)
-    fin_kernel<K, true><<<dim3(ngw + ncw, c->B), FT<K>::NT, lds, s>>>(
-        theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
-        std::max(h.n_sp, 1), ngw, c->eps, nth, S, c->nth_add, nullptr, nullptr, 0);
+    upd_kernel<K, true><<<dim3(nthw + ncw, c->B), UPD_NT, 0, s>>>(
+        theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
+        nth, S, c->nth_add, nullptr, nullptr, 0);
   else
-    fin_kernel<K, false><<<dim3(ngw + ncw + nqc, c->B), FT<K>::NT, lds, s>>>(
-        theta, pr, c->pold, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
-        std::max(h.n_sp, 1), ngw, c->eps, nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg);
+    upd_kernel<K, false><<<dim3(nthw + ncw + nqc, c->B), UPD_NT, 0, s>>>(
+        theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
+        nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -1790,6 +1622,8 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   if ((rc = upload(&sd.prow_ptr, h.prow_ptr))) return rc;
   if ((rc = upload(&sd.prow_gene, h.prow_gene))) return rc;
   if ((rc = upload(&sd.sp_desc, h.sp_desc))) return rc;
+  if ((rc = upload(&sd.row_y, h.row_y))) return rc;
+  if ((rc = upload(&sd.yptr, h.yptr))) return rc;
   for (int g = 0; g < 2; ++g) {
     if ((rc = upload(&sd.sku[g], h.sk_udesc[g]))) return rc;
     if ((rc = upload(&sd.skr[g], h.sk_urec[g]))) return rc;
@@ -1837,13 +1671,14 @@ int mmsbm_set_workspace(mmsbm_ctx* c, void* ws, int64_t bytes) {
   c->cbuf = (double*)(c->ws + L.cbuf);
   c->prows = (double*)(c->ws + L.prows);
   c->spart = (double*)(c->ws + L.spart);
-  c->pold = (double*)(c->ws + L.pold);
+  c->gx = (double*)(c->ws + L.gx);
   c->partL = (double*)(c->ws + L.partL);
   c->nth_tmp = (double*)(c->ws + L.nth);
   c->S_tmp = (double*)(c->ws + L.S);
-  // the c vector's last slot (stream-1/2 padding rows read it) and the S partials stay zero
+  // small-K: the c vector's last slot (stream-1/2 padding rows read it) and the S partials stay
+  // zero; large-K: Y and the S partials start zeroed (every word read is written each iteration)
   HIP_TRY(hipMemset(c->ws + L.cbuf, 0, L.prows - L.cbuf));
-  HIP_TRY(hipMemset(c->ws + L.spart, 0, L.pold - L.spart));
+  HIP_TRY(hipMemset(c->ws + L.spart, 0, L.gx - L.spart));
   HIP_TRY(hipDeviceSynchronize());
   return MMSBM_OK;
 }
@@ -2089,7 +1924,8 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[11] = h.small ? h.n_units : (int64_t)(h.n_wg_a + h.n_wg_b) * NW;
   info[12] = c->sets[which].ncu;
   info[13] = c->sets[which].unit_target;
-  info[14] = info[15] = 0;
+  info[14] = h.n_y;
+  info[15] = 0;
   return MMSBM_OK;
 }
 

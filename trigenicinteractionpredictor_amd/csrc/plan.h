@@ -16,6 +16,13 @@
 // Row record (int4): (i, j, k, w); stream 0: w = n_r (0 on padding rows); streams 1, 2: w = the
 // stream-0 row of the same observation (its c = n / d lives there), padding rows: w = n_rows0 (a
 // slot that always holds 0).
+//
+// Large-K EM plans (mmsbm.hip) hold stream 0 only: the pass over the stream-0 rows writes, per
+// observation, the j-slot and k-slot contributions c Z and c Z' (K words each) into Y ENTRIES, and
+// the gene kernel sums each gene's entries.  The entries of one gene are contiguous: ordered by
+// gene, then slot (1, 2), rating and link order; `yptr` [P + 1] delimits them and `row_y`
+// [n_rows0][2] names the slot-1 / slot-2 entry of every stream-0 row (n_y on padding rows: a
+// dummy entry nobody reads).
 #pragma once
 
 #include <algorithm>
@@ -68,6 +75,10 @@ struct Plan {
   std::vector<int> wg_ustart;      // [n_wg + 1] units of each workgroup (rounds of NW)
   std::vector<int> row12;          // [n_rows0][2] the observation's stream-1 / stream-2 row
                                    // (relative to n_rows0; -1 on padding rows)
+  // large-K EM plans only: Y entries (see the header)
+  std::vector<int> row_y;          // [n_rows0][2] slot-1 / slot-2 entry of each stream-0 row
+  std::vector<int> yptr;           // [P + 1] entries of each gene
+  long long n_y = 0;               // 2 x observations
   int rounds_a = 1, rounds_b = 1;  // unit rounds per workgroup (stream 0 / streams 1, 2)
   long long n_units = 0;
   // slot layout the small-K kernels read (make_slots below); group 0 = stream 0 (pass A), group 1 =
@@ -204,7 +215,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   pl.gu = std::max(1, std::min(gu, GU));
   pl.R = R;
   pl.P = P;
-  pl.streams = em ? 3 : 1;
+  pl.streams = (em && small) ? 3 : 1;  // large-K EM plans: stream 0 + Y entries
   pl.small = small;
   // observations of each rating in link order
   std::vector<std::vector<int>> obs(R);
@@ -455,6 +466,21 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   }
   pl.n_wg_b = (int)pl.wg_code.size() - pl.n_wg_a;
   pl.wg_gene.push_back((int)pl.vgenes.size());
+  if (em && !small) {
+    // Y entries: every observation's slot-1 and slot-2 gene, grouped by gene (counting sort,
+    // stable over slot, rating, link order)
+    pl.yptr.assign((size_t)P + 1, 0);
+    for (int s = 1; s <= 2; ++s)
+      for (int r = 0; r < R; ++r)
+        for (int e : obs[r]) pl.yptr[(size_t)ids[(size_t)e * 3 + s] + 1]++;
+    for (int g = 0; g < P; ++g) pl.yptr[g + 1] += pl.yptr[g];
+    pl.n_y = pl.yptr[P];
+    std::vector<int> pos(pl.yptr.begin(), pl.yptr.end() - 1);
+    pl.row_y.assign((size_t)2 * pl.n_rows0, (int)pl.n_y);
+    for (int s = 1; s <= 2; ++s)
+      for (int r = 0; r < R; ++r)
+        for (int e : obs[r]) pl.row_y[(size_t)2 * row0[r][e] + (s - 1)] = pos[ids[(size_t)e * 3 + s]]++;
+  }
   for (auto& rec : pl.rows)
     if (rec.w == -2) rec.w = (int)pl.n_rows0;  // padding rows of streams 1, 2: the zero c slot
   if (small) {

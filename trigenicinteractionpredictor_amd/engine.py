@@ -24,7 +24,13 @@ def _host_ptr(a: np.ndarray):
 
 
 class EMEngine:
-    KERNELS = ("pass_a", "pass_b", "fin")
+    KERNELS = ("pass_a", "pass_b", "fin")   # kernel ids of include/mmsbm.h's timing calls
+    # what each id launches, by plan family (plan_info "small_k"): the large-K kernels (0) run
+    # pass A, the gene kernel and the update; the small-K plan (1) pass A, pass B and fin; the
+    # fused small-K plan (2) one fused E-step and fin
+    LABELS = {0: {"pass_a": 0, "gene": 1, "fin": 2},
+              1: {"pass_a": 0, "pass_b": 1, "fin": 2},
+              2: {"fused": 0, "fin": 2}}
 
     def __init__(self, K: int, P: int, B: int = 1, R: int = 2, eps: float = 1e-10, device=None):
         if not torch.cuda.is_available():
@@ -78,7 +84,7 @@ class EMEngine:
         _lib.check(self.lib.mmsbm_plan_info(self.ctx, which, v))
         keys = ("observations", "rows", "rows_stream0", "wg_stream0", "wg_stream12", "wg_spartial",
                 "partial_rows", "genes_per_wg_max", "v_genes", "partial_rows_stream0", "small_k",
-                "units", "plan_cus", "unit_target")
+                "units", "plan_cus", "unit_target", "y_entries")
         return dict(zip(keys, [int(x) for x in v]))
 
     # ------------------------------------------------------------ parameters
@@ -153,7 +159,7 @@ class EMEngine:
     def timing_result(self, kernel: str = "pass_a"):
         """-> (summed device ms, launches) of one kernel since timing(stride)."""
         tot, cnt = ctypes.c_double(), ctypes.c_int64()
-        _lib.check(self.lib.mmsbm_timing_result(self.ctx, self.KERNELS.index(kernel),
+        _lib.check(self.lib.mmsbm_timing_result(self.ctx, self._kid(kernel),
                                                 ctypes.byref(tot), ctypes.byref(cnt)))
         return tot.value, cnt.value
 
