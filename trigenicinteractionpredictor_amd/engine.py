@@ -143,11 +143,23 @@ class EMEngine:
         return out[:, :n].cpu().numpy()
 
     # ---------------------------------------------------------- measurement
+    def kernels(self) -> dict:
+        """{label: kernel id} of the kernels one iteration launches, in launch order (LABELS)."""
+        return dict(self.LABELS[self.plan_info(_lib.SET_TRAIN)["small_k"]])
+
+    def _kid(self, kernel) -> int:
+        if kernel in self.KERNELS:
+            return self.KERNELS.index(kernel)
+        for labels in self.LABELS.values():
+            if kernel in labels:
+                return labels[kernel]
+        raise KeyError(kernel)
+
     def time_kernel(self, kernel: str, n: int = 50, stream=None) -> float:
-        """Average device ms of n back-to-back launches of one kernel of the iteration
-        ("pass_a", "pass_b", "fin"); the parameters are unchanged."""
+        """Average device ms of n back-to-back launches of one kernel of the iteration (a label
+        of kernels() or an id name of KERNELS); the parameters are unchanged."""
         ms = ctypes.c_double()
-        _lib.check(self.lib.mmsbm_time_kernel(self.ctx, self.KERNELS.index(kernel), _ptr(self.theta),
+        _lib.check(self.lib.mmsbm_time_kernel(self.ctx, self._kid(kernel), _ptr(self.theta),
                                               _ptr(self.pr), int(n), self._stream(stream),
                                               ctypes.byref(ms)))
         return ms.value
