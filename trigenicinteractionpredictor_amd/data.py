@@ -172,6 +172,9 @@ def _write_fold_numpy(spec: FoldSpec, train_path: str, test_path: str):
     width = len(gene_name(spec.P - 1))
 
     def dump(path, tri):
+        if tri.shape[0] == 0:                      # (test_frac 0: an empty test file)
+            open(path, "w").close()
+            return
         r = (rs.random(tri.shape[0]) < spec.pos_frac).astype(np.int64)
         names = np.char.add("g", np.char.zfill(tri.astype(str), width - 1))
         lines = np.char.add(np.char.add(np.char.add(names[:, 0], "_"),
