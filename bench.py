@@ -118,8 +118,8 @@ def spawn_ranks(n):
 KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, Z', d, c, the j / k Y entries, M0 "
                           "partial rows; FP64 MFMA)",
                 "gene": "gene_kernel<%d> (X0 contractions on FP64 MFMA, S partials, Y entry sums)",
-                "fused": "sk_pass_kernel<%d, SK_U> (fused E-step, all 3 streams: V, Z, d, c, M, X; "
-                         "stream-0 S partials; FP64 MFMA)",
+                "fused": "fused E-step: sky_pass_kernel<%d> (SK_Y, stream 0: V, Z, Z', d, c, Y entries, "
+                         "M, X, S partials) / sk_pass_kernel<K, SK_U> (3 streams); FP64 MFMA",
                 "pass_b": "sk_pass_kernel<%d, SK_B> (streams 1/2: M1, M2, X)",
                 "fin": "fin: sk_fin_kernel<%d> / upd_kernel (theta and p update)"}
 
@@ -135,6 +135,18 @@ def kernel_work(plan, K, P, R, B, E_obs):
     prow0 = plan["partial_rows_stream0"]
     genes_a = plan["v_genes"]
     params = 8.0 * (P * K + R * K3)
+    if plan.get("small_k") == 3:
+        # the stream-0 small-K E-step with Y entries (csrc/sk.h SK_Y): per observation Z, Z', M
+        # (2K^2 each) and d; per stretch a V table and an X contraction, per stretch an S update;
+        # bytes: records + their Y entry indices, 2K words of Y entries per observation, X partials,
+        # S partials.  fin: per gene its X partial rows and Y entries, per cell the S partials.
+        wga = plan["wg_stream0"]
+        n_y = plan.get("y_entries", 2 * E_obs)
+        u_fl = E_obs * (6.0 * K2 + 2.0 * K) + prow0 * 3 * 2.0 * K3
+        u_by = 24.0 * rows0 + 8.0 * K * n_y + 8.0 * K * prow0 + 8.0 * K3 * wga + params
+        f_fl = 1.0 * prow0 * K + 1.0 * n_y * K + R * K3 * wga + 3.0 * P * K + 3.0 * R * K3
+        f_by = 8.0 * K * prow0 + 8.0 * K * n_y + 8.0 * K3 * wga + 2 * params + 4.0 * 8 * P
+        return {"fused": (u_fl * B, u_by * B), "fin": (f_fl * B, f_by * B)}
     if plan.get("small_k") == 2:
         # the fused small-K E-step (csrc/sk.h SK_U): every stream's observations get Z, d, c and
         # M (each stream forms its own c); per stretch of any stream a V table and an X

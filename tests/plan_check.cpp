@@ -20,6 +20,39 @@ static int fail(const char* what, long long a = 0, long long b = 0) {
   return 1;
 }
 
+// Y entries (large-K EM plans and small-K SK_Y plans, stream 0 only): yptr tiles
+// [0, n_y = 2 x observations), an entry of gene g's range is named by exactly one (stream-0 row,
+// slot 1 / 2) whose slot gene is g, and padding rows name the dummy entry n_y
+static int check_y(const Plan& pl, int P, long long n_obs) {
+
+  if (pl.n_y != 2 * n_obs || (int)pl.yptr.size() != P + 1 || pl.yptr[0] != 0 || pl.yptr[P] != pl.n_y)
+    return fail("yptr", pl.n_y, 2 * n_obs);
+  if ((long long)pl.row_y.size() != 2 * pl.n_rows0) return fail("row_y size");
+  {
+    std::vector<int> owner(pl.n_y, -1), hits(pl.n_y, 0);
+    for (int g = 0; g < P; ++g) {
+      if (pl.yptr[g + 1] < pl.yptr[g]) return fail("yptr order", g);
+      for (int e = pl.yptr[g]; e < pl.yptr[g + 1]; ++e) owner[e] = g;
+    }
+    for (long long q = 0; q < pl.n_rows0; ++q) {
+      const I4& x = pl.rows[q];
+      for (int k = 0; k < 2; ++k) {
+        const int e = pl.row_y[2 * q + k];
+        if (x.w <= 0) {
+          if (e != pl.n_y) return fail("row_y padding", q, e);
+          continue;
+        }
+        if (e < 0 || e >= pl.n_y) return fail("row_y range", q, e);
+        if (owner[e] != (k == 0 ? x.y : x.z)) return fail("row_y gene", q, e);
+        hits[e]++;
+      }
+    }
+    for (long long e = 0; e < pl.n_y; ++e)
+      if (hits[e] != 1) return fail("y entry coverage", e, hits[e]);
+  }
+  return 0;
+}
+
 // Small-K plan: units of at most GU stretches and LCAP_SK chunks covering every chunk once, their
 // descriptors (stretch starts, pivot genes, partial rows), workgroup unit ranges of one
 // (stream, rating), the c scatter map row12, and the S-partial workgroup ranges.
@@ -67,8 +100,9 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
     if (covered[c] != 1) return fail("chunk coverage", c, covered[c]);
   // row12: the stream-1 / stream-2 rows of each real stream-0 row hold the same triple and point
   // back at it; padding rows map to -1
-  if ((long long)pl.row12.size() != 2 * pl.n_rows0) return fail("row12 size");
-  for (long long q = 0; q < pl.n_rows0; ++q) {
+  const bool yent = !pl.row_y.empty();
+  if (!yent && (long long)pl.row12.size() != 2 * pl.n_rows0) return fail("row12 size");
+  for (long long q = 0; q < (yent ? 0 : pl.n_rows0); ++q) {
     const I4& x = pl.rows[q];
     for (int k = 0; k < 2; ++k) {
       const int t = pl.row12[2 * q + k];
@@ -115,7 +149,22 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
     }
   }
   if (units_seen != pl.n_units) return fail("slot units", units_seen, pl.n_units);
-  {
+  if (yent) {  // SK_Y: the slot-major urow12 holds each stream-0 row's Y entries
+    if (int rc = check_y(pl, P, pl.n_obs)) return rc;
+    if (pl.n_wg_b != 0 || (long long)pl.rows.size() != pl.n_rows0) return fail("SK_Y streams", pl.n_wg_b);
+    const int L = pl.sk_L[0];
+    const int per = NW * pl.rounds_a;
+    for (long long slot = 0; slot < pl.sk_slots[0]; ++slot) {
+      const int* d = &pl.sk_udesc[0][(size_t)slot * UD];
+      if (d[D_NST] == 0) continue;
+      const int u = pl.wg_ustart[(int)(slot / per)] + (int)(slot % per);
+      const int* du = &pl.udesc[(size_t)u * UD];
+      for (int i = 0; i < 4 * d[D_END]; ++i)
+        for (int k = 0; k < 2; ++k)
+          if (pl.sk_urow12[((size_t)slot * 4 * L + i) * 2 + k] != pl.row_y[(4LL * du[0] + i) * 2 + k])
+            return fail("SK_Y urow12", slot, i);
+    }
+  } else {
     const int La = pl.sk_L[0], Lb = pl.sk_L[1];
     for (long long i = 0; i < pl.sk_slots[0] * 4 * La; ++i) {
       const I4& a = pl.sk_urec[0][i];
@@ -153,10 +202,12 @@ int main() {
       if (scanf("%d", &counts[e * R + r]) != 1) return fail("counts");
   }
   // gcap <= 0: the small-K plans of sk.h (sp_rows = their wg_target): 0 = 4 stretches per unit
-  // (K 11-12), -3 = 8 (K <= 10); fill-packed (the fused launch) -1 = 8, -2 = 4
-  const bool small = gcap <= 0, fill = gcap == -1 || gcap == -2;
+  // (K 11-12), -3 = 8 (K <= 10); fill-packed (the fused launch) -1 = 8, -2 = 4; -4 = fill-packed
+  // stream-0 plans with Y entries (SK_Y), 8 stretches
+  const bool small = gcap <= 0, fill = gcap == -1 || gcap == -2 || gcap == -4, yent = gcap == -4;
   const int gu = (gcap == 0 || gcap == -2) ? 4 : 8;
-  const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill, gu)
+  const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill, gu,
+                                85, yent)
                         : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows);
   if (fill) {  // every unit but the last of its (stream, rating) section is full: LCAP_SK chunks or GU stretches
     for (long long u = 0; u + 1 < pl.n_units; ++u) {
@@ -278,35 +329,8 @@ int main() {
     }
     if (q1 > q0 && at != q1) return fail("sp end", r, at);
   }
-  // 6. large-K EM plans hold stream 0 only; Y entries: yptr tiles [0, n_y = 2 x observations),
-  //    an entry of gene g's range is named by exactly one (stream-0 row, slot 1 / 2) whose slot gene
-  //    is g, and padding rows name the dummy entry n_y
+  if (int rc = check_y(pl, P, n_obs)) return rc;
   if (pl.n_wg_b != 0 || (long long)pl.rows.size() != pl.n_rows0) return fail("large-K streams", pl.n_wg_b);
-  if (pl.n_y != 2 * n_obs || (int)pl.yptr.size() != P + 1 || pl.yptr[0] != 0 || pl.yptr[P] != pl.n_y)
-    return fail("yptr", pl.n_y, 2 * n_obs);
-  if ((long long)pl.row_y.size() != 2 * pl.n_rows0) return fail("row_y size");
-  {
-    std::vector<int> owner(pl.n_y, -1), hits(pl.n_y, 0);
-    for (int g = 0; g < P; ++g) {
-      if (pl.yptr[g + 1] < pl.yptr[g]) return fail("yptr order", g);
-      for (int e = pl.yptr[g]; e < pl.yptr[g + 1]; ++e) owner[e] = g;
-    }
-    for (long long q = 0; q < pl.n_rows0; ++q) {
-      const I4& x = pl.rows[q];
-      for (int k = 0; k < 2; ++k) {
-        const int e = pl.row_y[2 * q + k];
-        if (x.w <= 0) {
-          if (e != pl.n_y) return fail("row_y padding", q, e);
-          continue;
-        }
-        if (e < 0 || e >= pl.n_y) return fail("row_y range", q, e);
-        if (owner[e] != (k == 0 ? x.y : x.z)) return fail("row_y gene", q, e);
-        hits[e]++;
-      }
-    }
-    for (long long e = 0; e < pl.n_y; ++e)
-      if (hits[e] != 1) return fail("y entry coverage", e, hits[e]);
-  }
   printf("ok %zu %d %d %lld %d\n", pl.rows.size(), n_wg * NW, n_wg, pl.n_prows, pl.n_sp);
   return 0;
 }

@@ -62,6 +62,10 @@ def _links(P, E, seed, R=2, hub=0.0, multi=0.05, both=0.03):
     (1500, 20000, (1, 1), -1, 1024, 0.0),      # fold0-like degree
     (40, 600, (1, 1), -1, 1024, 0.0),          # few genes: long runs
     (1500, 20000, (1, 1), -2, 1024, 0.0),      # 4 stretches (K = 11, 12)
+    # fill-packed stream-0 plans with Y entries (gcap -4: SK_Y, the fused small-K E-step of round 4)
+    (300, 5000, (1, 1), -4, 1024, 30.0),       # hub genes
+    (1500, 20000, (3840, 3840), -4, 1024, 0.0),  # fold0-like degree, 15 units per CU
+    (40, 600, (64, 64), -4, 1024, 0.0),        # few genes: long runs
 ])
 def test_plan_invariants(plan_check, P, E, units, gcap, sp_rows, hub):
     links = _links(P, E, seed=P + E, hub=hub)

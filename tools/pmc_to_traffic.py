@@ -13,7 +13,7 @@ import sys
 
 NAMES = {"pass_kernel<%d, 0>": "pass_a", "gene_kernel<%d>": "gene", "upd_kernel<%d, false>": "fin",
          # small-K kernels (csrc/sk.h), labelled as EMEngine.LABELS names them
-         "sk_pass_kernel<%d, 3>": "fused", "sk_pass_kernel<%d, 0>": "pass_a",
+         "sky_pass_kernel<%d>": "fused", "sk_pass_kernel<%d, 3>": "fused", "sk_pass_kernel<%d, 0>": "pass_a",
          "sk_pass_kernel<%d, 2>": "pass_b", "sk_fin_kernel<%d, false>": "fin"}
 
 

@@ -1102,6 +1102,7 @@ struct mmsbm_ctx {
   int gcap = 0;                  // most pivot genes per stream-0 workgroup (<= KT<K>::GMAX)
   bool sk = false;               // K <= 12: the small-K kernels of sk.h (MMSBM_SK=0: the large-K ones)
   bool sk_fused = false;         // small-K: one fused E-step launch (SK_U) instead of pass A + pass B
+  bool sk_y = false;             // small-K fused: the stream-0 E-step with Y entries (SK_Y, default)
   SetDev sets[2];
   int* deg = nullptr;            // device, owned
   std::vector<int> deg_host;
@@ -1150,8 +1151,10 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   if (c->sk) {
     // small-K: c at the stream-1/2 rows, X partials (K per partial row), S partials (K^3 per
     // stream-0 workgroup), likelihood partials, fin's sums-out scratch
+    // (SK_Y: the Y entries instead of c)
     L.cbuf = off;
-    off += align_up(B * std::max<long long>(tr.sk_slots[1] * 4 * tr.sk_L[1], 1) * 8);
+    off += align_up(c->sk_y ? B * (tr.n_y + 1) * c->K * 8
+                            : B * std::max<long long>(tr.sk_slots[1] * 4 * tr.sk_L[1], 1) * 8);
     L.prows = off;
     off += align_up(B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
     L.spart = off;
@@ -1314,6 +1317,12 @@ int launch_sk_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const
     sk_pass_kernel<K, SK_B><<<dim3(h.n_wg_b, c->B), NT, T::LDS_B, s>>>(
         sd.skr[1], sd.sku[1], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, h.n_wg_a,
         h.sk_L[1], c->P, c->R, n_cb, h.n_prows, h.n_wg_b, c->eps, nullptr, nullptr, 0);
+  } else if (mode == PASS_A && c->sk_y) {  // SK_Y: the stream-0 E-step with Y entries
+    if (h.n_wg_a == 0) return MMSBM_OK;
+    if ((rc = lds_opt_in(c, 9, &sky_pass_kernel<K>, SKY<K>::LDS))) return rc;
+    sky_pass_kernel<K><<<dim3(h.n_wg_a, c->B), NT, SKY<K>::LDS, s>>>(
+        sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, sec, h.sk_L[0], c->P, c->R,
+        h.n_y, h.n_prows, h.n_wg_a, c->eps);
   } else if (mode == PASS_A && c->sk_fused) {  // the fused E-step: every stream in one launch
     if (h.n_wg_a + h.n_wg_b == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 7, &sk_pass_kernel<K, SK_U>, T::LDS_U))) return rc;
@@ -1342,8 +1351,10 @@ int launch_sk_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nt
                   hipStream_t s) {
   const SetDev& sd = c->sets[MMSBM_SET_TRAIN];
   const auto& h = sd.h;
-  const int ngw = (c->P * K + SKF_NT - 1) / SKF_NT;
+  // gene workgroups: threads per (gene, component), or (SK_Y) one wave per gene
+  const int ngw = c->sk_y ? (c->P + SKF_NT / 64 - 1) / (SKF_NT / 64) : (c->P * K + SKF_NT - 1) / SKF_NT;
   const int ncw = (K * K * K + SKF_CW - 1) / SKF_CW;
+  const double* yb = c->sk_y ? c->cbuf : nullptr;
   SpRange spr{};
   for (int r = 0; r < c->R; ++r) {
     spr.lo[r] = h.sp_lo[r];
@@ -1353,11 +1364,12 @@ int launch_sk_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nt
   if (sums)
     sk_fin_kernel<K, true><<<dim3(ngw + ncw, c->B), SKF_NT, 0, s>>>(
         theta, pr, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
-        std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, nullptr, nullptr, 0);
+        std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, nullptr, nullptr, 0, yb, sd.yptr, h.n_y);
   else
     sk_fin_kernel<K, false><<<dim3(ngw + ncw + nqc, c->B), SKF_NT, 0, s>>>(
         theta, pr, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
-        std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg);
+        std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg, yb, sd.yptr,
+        h.n_y);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -1542,6 +1554,15 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
       c->ws_bytes = 0;
     }
     c->sk_fused = fused;
+    const char* y = getenv("MMSBM_SK_Y");  // SK_Y (default); 0: the three-stream fused E-step (SK_U)
+    const bool sky = fused && !(y && y[0] == '0');
+    if (sky != c->sk_y) {  // the plans hold different streams: set links again
+      DeviceGuard g(c->device);
+      for (auto& sd : c->sets) sd.release();
+      c->ws = nullptr;
+      c->ws_bytes = 0;
+    }
+    c->sk_y = sky;
   }
   ++c->gen;
   c->attr = 0;      // the dynamic-LDS opt-ins are per kernel, and the kernels depend on K
@@ -1598,7 +1619,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   if (const char* e = getenv("MMSBM_SK_RHO")) rho = std::max(10, std::min(100, atoi(e)));
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
                            c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, 1024, c->sk_fused,
-                           mmsbm_plan::sk_gu(c->K), rho);
+                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y);
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
   sd.unit_target = c->sk_fused ? units_a : 0;
@@ -1920,7 +1941,7 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[9] = h.prow_ptr.empty() ? 0 : h.prow_ptr[(size_t)h.R * (h.P + 1)];  // stream-0 partial rows
   info[7] = h.small ? h.gu : h.gmax;
   info[8] = h.small ? info[9] : (int64_t)h.vgenes.size();  // small-K: one V table per stream-0 stretch
-  info[10] = h.small ? (c->sk_fused ? 2 : 1) : 0;
+  info[10] = h.small ? (c->sk_y ? 3 : c->sk_fused ? 2 : 1) : 0;
   info[11] = h.small ? h.n_units : (int64_t)(h.n_wg_a + h.n_wg_b) * NW;
   info[12] = c->sets[which].ncu;
   info[13] = c->sets[which].unit_target;

@@ -191,6 +191,13 @@ inline void make_slots(Plan& pl) {
         }
       }
   }
+  if (!pl.row_y.empty()) {  // SK_Y: each slot row's Y entries (n_y: padding, never a real store)
+    const int L = pl.sk_L[0];
+    pl.sk_urow12.assign((size_t)pl.sk_slots[0] * 4 * L * 2, (int)pl.n_y);
+    for (long long q = 0; q < pl.n_rows0; ++q)
+      if (pos[q] >= 0)
+        for (int k = 0; k < 2; ++k) pl.sk_urow12[(size_t)2 * pos[q] + k] = pl.row_y[(size_t)2 * q + k];
+  }
   if (!pl.row12.empty()) {
     const int L = pl.sk_L[0];
     pl.sk_urow12.assign((size_t)pl.sk_slots[0] * 4 * L * 2, -1);
@@ -210,12 +217,15 @@ inline void make_slots(Plan& pl) {
 // K^3 partial, so large K wants more rows per partial).
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
-                  int wg_target = 1024, bool fill = false, int gu = GU, int rho_pct = 85) {
+                  int wg_target = 1024, bool fill = false, int gu = GU, int rho_pct = 85,
+                  bool yent = false) {
   Plan pl;
   pl.gu = std::max(1, std::min(gu, GU));
   pl.R = R;
   pl.P = P;
-  pl.streams = (em && small) ? 3 : 1;  // large-K EM plans: stream 0 + Y entries
+  // large-K EM plans, and small-K EM plans with `yent` (sk.h SK_Y): stream 0 + Y entries
+  const bool ymode = em && (!small || yent);
+  pl.streams = (em && !ymode) ? 3 : 1;
   pl.small = small;
   // observations of each rating in link order
   std::vector<std::vector<int>> obs(R);
@@ -443,7 +453,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
           q = q1;
         }
         pl.n_rows0 = (long long)pl.rows.size();
-        if (small && em) pl.row12.resize((size_t)2 * pl.n_rows0, -1);
+        if (small && em && !ymode) pl.row12.resize((size_t)2 * pl.n_rows0, -1);
       } else {
         // c index of every row of this stream section
         size_t rr = (size_t)row_base;
@@ -466,7 +476,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   }
   pl.n_wg_b = (int)pl.wg_code.size() - pl.n_wg_a;
   pl.wg_gene.push_back((int)pl.vgenes.size());
-  if (em && !small) {
+  if (ymode) {
     // Y entries: every observation's slot-1 and slot-2 gene, grouped by gene (counting sort,
     // stable over slot, rating, link order)
     pl.yptr.assign((size_t)P + 1, 0);

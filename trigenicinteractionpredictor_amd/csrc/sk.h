@@ -591,10 +591,359 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// SK_Y (round 4, the default small-K E-step): ONE launch over the stream-0 slots only.  The j- and
+// k-slot sums of an observation factor through its stream-0 pivot's V table (mmsbm.hip header,
+// tests/pivot_model.py::iterate_y):
+//   sum_ah T = th_j[b] Z[b],  Z[b] = sum_h V_i[b][h] th_k[h];   sum_ab T = th_k[h] Z'[h],
+//   Z'[h] = sum_b th_j[b] V_i[b][h]
+// so per chunk the wave forms Z and Z' (two 4x4x4 MFMA chains over the V table, read row- and
+// column-wise from its slot), d = eps + th_j . Z, c = n / d, writes the Y entries c Z (gene j)
+// and c Z' (gene k) and accumulates M^0 += c th_j (x) th_k.  Streams 1 and 2 — their records,
+// their theta gathers, V tables, c and M work and their X contractions — do not exist.  At the
+// unit's end: X^0 of its stretches and the workgroup's S partial, as SK_U does for stream 0;
+// sk_fin_kernel then adds each gene's Y entries (Plan::yptr) to its X^0 partial rows.
+// c is computed per sub-batch of 4 chunks (16 observations, one lane each), so only 4 chunks'
+// Z / Z' stay live in registers between phase 1 (Z, Z', d) and phase 2 (c, Y, M).
+// ------------------------------------------------------------------------------------------
+template <int K>
+struct SKY {
+  using T = SKT<K>;
+  // per wave: slots, the block's (u, v) genes, pivot rows, the block's Y entries, one transpose
+  // buffer, d / c words
+  static constexpr int WAVE = T::GUK * T::SLOT + SK_ROWS + T::THL + SK_ROWS + 64 + SK_ROWS;
+  static constexpr int LDS = (T::PSD + NW * WAVE) * 8;
+  static_assert(LDS <= 80 * 1024, "two SK_Y workgroups per CU");
+  // the unguarded Z' operand reads (rows b < 4 NG of the last slot, columns up to 15) stay inside
+  // the wave's slots, records and pivot rows (finite words)
+  static_assert((T::GUK - 1) * T::SLOT + (4 * T::NG - 1) * K + 15 < T::GUK * T::SLOT + SK_ROWS + T::THL,
+                "Z' reads past the wave's slots");
+};
+
+template <int K>
+__global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
+    const int4* __restrict__ urec, const int* __restrict__ udesc, const int2* __restrict__ urowy,
+    const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ ybuf,
+    double* __restrict__ xpart, double* __restrict__ spart, SkSec sec, int L, int P, int R,
+    long long n_y, long long n_prows, int n_wg, double eps) {
+  using T = SKT<K>;
+  using Y = SKY<K>;
+  constexpr int NG = T::NG, K2 = T::K2, K3 = T::K3, NCT = T::NCT, NCG = T::NCG, SLOT = T::SLOT;
+  constexpr int GUK = T::GUK, NT2 = T::NT2;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3, col = lane & 15;
+  const int w = blockIdx.x, b = blockIdx.y;
+  int sr = 0;  // this workgroup's (stream 0, rating) section, from the launch arguments alone
+#pragma unroll
+  for (int i = 0; i < MAX_R - 1; ++i)
+    if (i + 1 < R && w >= sec.wg_end[i]) sr = i + 1;
+  const int r = __builtin_amdgcn_readfirstlane(sr);
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+  const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
+  double* PV = smem;  // P^0_r[z][cell] (cell = x K + y), zero past K^3
+  double* wl = smem + T::PSD + wv * Y::WAVE;
+  double* MSl = wl;                                        // GUK slots: V, then M
+  int2* REC = reinterpret_cast<int2*>(wl + GUK * SLOT);    // the block's (u, v) genes
+  double* THl = wl + GUK * SLOT + SK_ROWS;                 // pivot theta rows [GUK][4 NG]
+  int2* YE = reinterpret_cast<int2*>(THl + T::THL);        // the block's Y entries (slot 1, slot 2)
+  double* TRl = THl + T::THL + SK_ROWS;                    // the Z / Z' operand transpose
+  double* DL = TRl + 64;                                   // d, then c, per observation
+  double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * K;
+  double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
+  Stamp st_{};
+  st_.mark(0);
+
+  // P^0_r once per workgroup (plain copy: the pivot slot is slot 0)
+  double pvv[T::NPV];
+#pragma unroll
+  for (int i = 0; i < T::NPV; ++i) {
+    const int e = tid + NT * i;
+    const double v = p[e < K3 ? e : 0];
+    pvv[i] = e < K3 ? v : 0.0;
+  }
+
+  const long long slot = (long long)w * NW + wv;
+  struct Unit {
+    int nst, c1, ds[GUK], prow[NT2];
+    double tv[NT2][NG];
+  };
+  struct Blk {
+    int4 rv;
+    int2 ry;
+  };
+  auto load_block = [&](int bi, Blk& bk) {
+    const int idx = SK_ROWS * bi + lane;
+    const long long row = slot * 4 * L + (idx < 4 * L ? idx : 4 * L - 1);
+    bk.rv = urec[row];
+    bk.ry = urowy[row];
+  };
+  int wlane = 0;
+  auto stage_block = [&](const Blk& bk) {
+    REC[lane] = make_int2(bk.rv.x, bk.rv.y);
+    wlane = bk.rv.w;
+    YE[lane] = bk.ry;
+  };
+  auto load_unit = [&](Unit& un) {
+    const int* __restrict__ d = udesc + slot * mmsbm_plan::UD;
+    un.nst = __builtin_amdgcn_readfirstlane(d[mmsbm_plan::D_NST]);
+    un.c1 = __builtin_amdgcn_readfirstlane(d[mmsbm_plan::D_END]);
+#pragma unroll
+    for (int t = 0; t < GUK; ++t) un.ds[t] = __builtin_amdgcn_readfirstlane(d[t]);
+#pragma unroll
+    for (int tt = 0; tt < NT2; ++tt) un.prow[tt] = d[mmsbm_plan::D_PROW + 4 * tt + hi];
+#pragma unroll
+    for (int tt = 0; tt < NT2; ++tt) {
+      const int glo = d[mmsbm_plan::D_GENE + 4 * tt + lo];
+#pragma unroll
+      for (int as = 0; as < NG; ++as) {
+        const int a1 = 4 * as + hi;
+        const double v1 = th[(size_t)glo * K + (a1 < K ? a1 : 0)];
+        un.tv[tt][as] = (4 * tt + lo < un.nst && a1 < K) ? v1 : 0.0;
+      }
+    }
+  };
+  Blk bk;
+  load_block(0, bk);
+  Unit un;
+  load_unit(un);
+#pragma unroll
+  for (int i = 0; i < T::NPV; ++i)
+    if (tid + NT * i < T::PSD) PV[tid + NT * i] = pvv[i];
+  stage_block(bk);
+  __syncthreads();  // P^0_r published (the V tables below read it)
+  st_.mark(6);
+
+  if (un.nst > 0) {
+    const int nst = un.nst;
+    const int c1 = un.c1;
+    st_.t[5] = (unsigned long long)c1;
+    st_.t[4] = (unsigned long long)nst;
+    const auto& ds = un.ds;
+    auto stretch_end = [&](int t) {
+      int e = c1;
+#pragma unroll
+      for (int i = 1; i < GUK; ++i)
+        if (t + 1 == i && i < nst) e = ds[i];
+      return e;
+    };
+    const int2* __restrict__ rec = REC;
+    const int colc = col < K ? col : K - 1;
+    const unsigned cb = (unsigned)colc * 8u;
+    const bool kcol = col < K;
+    const auto& tv = un.tv;
+    // ---- V_g[cell] = sum_a theta_g[a] P^0[a][cell] for the unit's genes into their slots (every
+    // word of the GUK slots written: zero past K^2 and for absent stretches); pivot theta rows to
+    // THl for the S pass
+#pragma unroll
+    for (int tt = 0; tt < NT2; ++tt) {
+      const bool live = tt == 0 || nst > 4 * tt;
+#pragma unroll
+      for (int cg = 0; cg < NCG; ++cg) {
+        const int cell = 4 * (4 * cg + blk) + lo;
+        double v = 0.0;
+        if (live) {
+#pragma unroll
+          for (int as = 0; as < NG; ++as)
+            v = mfma4(tv[tt][as], PV[(4 * as + hi < K ? 4 * as + hi : K - 1) * K2 + cell], v);
+        }
+        if (cell < SLOT) MSl[(4 * tt + hi) * SLOT + cell] = cell < K2 ? v : 0.0;
+      }
+#pragma unroll
+      for (int as = 0; as < NG; ++as)
+        if (blk == 0) THl[(4 * tt + lo) * 4 * NG + 4 * as + hi] = tv[tt][as];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wave_lds_sync();
+    st_.mark(1);
+
+    // Z operand V[b = col][h = 4 hs + hi] (zero for b >= K, h >= K); Z' operand V[b = 4 bs + hi]
+    // [h = col] (rows b >= K meet a zero theta_j; columns h >= K are never stored)
+    const double* __restrict__ vrow = MSl + col * K + hi;
+    const double* __restrict__ vcol = MSl + hi * K + col;
+    d4v m16 = d4v{0.0, 0.0, 0.0, 0.0};
+    int t = 0;
+    int send = stretch_end(0);
+    double vb[NG], vbt[NG];
+    auto load_v = [&](int tv_) {
+#pragma unroll
+      for (int hs = 0; hs < NG; ++hs) {
+        const double x = vrow[tv_ * SLOT + 4 * hs];
+        vb[hs] = kcol && 4 * hs + hi < K ? x : 0.0;
+        vbt[hs] = vcol[tv_ * SLOT + 4 * hs * K];
+      }
+    };
+    int vt = 0, vsend = send;
+    load_v(0);
+    for (int b0 = 0; b0 < c1; b0 += LC) {
+      const int nb = c1 - b0;
+      if (b0 > 0) {
+        wave_lds_sync();
+        stage_block(bk);
+        wave_lds_sync();
+      }
+      if (nb > LC) load_block(b0 / LC + 1, bk);
+      // ---- theta gathers straight into the MFMA operand registers (lane (obs hi, col): theta_j
+      // and theta_k of its observation, column col; col >= K a finite copy of column K - 1, masked
+      // where a product needs it), one sub-batch of 4 chunks ahead: two windows of 4 chunks live
+      // (the whole block's 32 values would spill)
+      const int2* __restrict__ recb = rec;
+      auto gather = [&](int q0, double (&ga)[4], double (&gv)[4]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          ga[u] = 0.0;
+          gv[u] = 0.0;
+          if (q0 + u < nb) {  // (uniform)
+            const int2 rh = recb[(q0 + u) * 4 + hi];
+            const char* __restrict__ thb = reinterpret_cast<const char*>(th);
+            ga[u] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
+            gv[u] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
+          }
+        }
+      };
+      double gaw[2][4], gvw[2][4];
+      gather(0, gaw[0], gvw[0]);
+#pragma unroll
+      for (int sb = 0; sb < LC / 4; ++sb) {
+        if (4 * sb < nb) {  // (uniform)
+          if (sb + 1 < LC / 4 && 4 * (sb + 1) < nb) gather(4 * (sb + 1), gaw[(sb + 1) & 1], gvw[(sb + 1) & 1]);
+          const double(&ga)[4] = gaw[sb & 1];
+          const double(&gv)[4] = gvw[sb & 1];
+          // ---- phase 1, 4 chunks: Z, Z' on MFMA (A = the transposed theta_k / theta_j tile through
+          // the wave's LDS, bank-swizzled; theta_j zeroed past K), d parked one word per observation
+          double zq[4], zpq[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = 4 * sb + u;
+            zq[u] = 0.0;
+            zpq[u] = 0.0;
+            if (q < nb) {
+              TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = gv[u];
+              wave_lds_sync();
+              double z = 0.0;
+#pragma unroll
+              for (int hs = 0; hs < NG; ++hs)
+                z = mfma4(TRl[16 * lo + ((4 * hs + hi) ^ (4 * (lo >> 1)))], vb[hs], z);
+              // (a wave's LDS accesses execute in order: the reads above precede this write)
+              TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = kcol ? ga[u] : 0.0;
+              wave_lds_sync();
+              double zp = 0.0;
+#pragma unroll
+              for (int bs = 0; bs < NG; ++bs)
+                zp = mfma4(TRl[16 * lo + ((4 * bs + hi) ^ (4 * (lo >> 1)))], vbt[bs], zp);
+              zq[u] = z;
+              zpq[u] = zp;
+              DL[q * 4 + hi] = row16_sum(ga[u] * z) + eps;
+              if (b0 + q + 1 == vsend) {  // the next stretch's V operands
+                ++vt;
+                vsend = stretch_end(vt);
+                if (vt < nst) load_v(vt);
+              }
+            }
+          }
+          wave_lds_sync();
+          // ---- c = n / d of the sub-batch's 16 observations (lanes 16 sb .. 16 sb + 15)
+          {
+            const double cl = sk_div((double)wlane, DL[lane]);
+            if ((lane >> 4) == sb) DL[lane] = cl;
+          }
+          wave_lds_sync();
+          // ---- phase 2: the Y entries c Z (gene j) and c Z' (gene k), M += c theta_j (x) theta_k
+          // (k = observation); a finished stretch's M row replaces its V table in slot t
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = 4 * sb + u;
+            if (q < nb) {
+              const double c = DL[q * 4 + hi];
+              const int2 ey = YE[q * 4 + hi];
+              if (kcol) {
+                yb[(size_t)ey.x * K + col] = c * zq[u];
+                yb[(size_t)ey.y * K + col] = c * zpq[u];
+              }
+              m16 = mfma16(ga[u], c * gv[u], m16);
+              if (b0 + q + 1 == send) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const int x = hi + 4 * i;
+                  if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
+                }
+                m16 = d4v{0.0, 0.0, 0.0, 0.0};
+                ++t;
+                send = stretch_end(t);
+              }
+            }
+          }
+        }
+      }
+    }
+    st_.mark(2);
+    // ---- X_q[z] = sum_cell P^0[z][cell] M_q[cell] for the unit's rows q
+    const int z = 4 * blk + lo;
+    const double* __restrict__ pz = PV + (z < K ? z : K - 1) * K2 + hi;
+#pragma unroll
+    for (int tt = 0; tt < NT2; ++tt) {
+      if (tt == 0 || nst > 4 * tt) {
+        double xa[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < NCT; ++ks)
+          xa[ks & 3] = mfma4(MSl[(4 * tt + lo) * SLOT + 4 * ks + hi], pz[4 * ks], xa[ks & 3]);
+        const double xacc = (xa[0] + xa[1]) + (xa[2] + xa[3]);
+        if (4 * tt + hi < nst && blk < NG && z < K) xb[(size_t)un.prow[tt] * K + z] = xacc;
+      }
+    }
+    st_.mark(3);
+  }
+
+  // ---- the workgroup's S partial in one pass over all its stretches (as SK_U's stream 0)
+  {
+    if (un.nst == 0) {
+#pragma unroll
+      for (int i = 0; i < (GUK * SLOT + 63) / 64; ++i)
+        if (lane + 64 * i < GUK * SLOT) MSl[lane + 64 * i] = 0.0;
+#pragma unroll
+      for (int i = 0; i < (T::THL + 63) / 64; ++i)
+        if (lane + 64 * i < T::THL) THl[lane + 64 * i] = 0.0;
+    }
+    __syncthreads();
+    double* __restrict__ out = spart + ((size_t)b * n_wg + w) * K3;
+    constexpr int NI = NG * NCG, NIW = (NI + NW - 1) / NW, QS = NW * GUK / 4;
+    double acc[NIW];
+#pragma unroll
+    for (int j = 0; j < NIW; ++j) acc[j] = 0.0;
+#pragma unroll 4
+    for (int qs = 0; qs < QS; ++qs) {
+      const int qw = (4 * qs) / GUK, qt = (4 * qs) % GUK + hi;
+      const double* __restrict__ wq = smem + T::PSD + qw * Y::WAVE;
+      const double* __restrict__ thq = wq + GUK * SLOT + SK_ROWS + qt * 4 * NG + lo;
+      const double* __restrict__ mq = wq + qt * SLOT + 4 * blk + lo;
+#pragma unroll
+      for (int j = 0; j < NIW; ++j) {
+        const int it = wv + NW * j;
+        if (j + 1 < NIW || it < NI) {
+          const int at = it / NCG, cg = it % NCG;
+          acc[j] = mfma4(thq[4 * at], mq[16 * cg], acc[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NIW; ++j) {
+      const int it = wv + NW * j;
+      const int a = 4 * (it / NCG) + hi, cell = 16 * (it % NCG) + 4 * blk + lo;
+      if (it < NI && a < K && cell < K2) out[a * K2 + cell] = acc[j];
+    }
+  }
+  st_.mark(7);
+  st_.flush(0, ((long long)b * gridDim.x + w) * NW + wv, lane);
+}
+
+// ------------------------------------------------------------------------------------------
 // sk_fin_kernel, grid (gene workgroups + cell workgroups + q workgroups, B), block 256.
 //   gene part: thread (g, x): X = sum over the 3 R (stream, rating) combos of g's X partials, in
 //     combo then row order (+ the joint model's pair sums); theta' = theta X / deg (:1016-1018)
-//     or, SUMS, nth = X.
+//     or, SUMS, nth = X.  SK_Y plans (ybuf set): one wave per gene; its Y entries (one contiguous
+//     block of K-word rows, Plan::yptr) are summed by lanes l < K floor(64 / K), lane l taking
+//     words l, l + LY, ... (component l mod K), the lanes of one component then added in lane
+//     order; lane x < K adds that to its X^0 partial rows (stream 0) and updates theta.
 //   cell part: 16 cells x 16 parts per workgroup: S_r[cell] = sum of the rating's S partials
 //     (one per stream-0 workgroup), parts combined in order; p' = p S / (eps + sum_r p S)
 //     (:1021-1028) in place, or, SUMS, S_out = S.
@@ -643,7 +992,8 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
     const int* __restrict__ prow_ptr, const double* __restrict__ spart, const int* __restrict__ deg,
     SpRange spr, int P, int R, long long n_prows, int n_wg_a, int n_gene_wg, double eps,
     double* __restrict__ nth_out, double* __restrict__ S_out, const double* __restrict__ nth_add,
-    const double* __restrict__ q_part, double* __restrict__ q_out, int n_qwg) {
+    const double* __restrict__ q_part, double* __restrict__ q_out, int n_qwg,
+    const double* __restrict__ ybuf, const int* __restrict__ yptr, long long n_y) {
   constexpr int K2 = K * K, K3 = K * K * K;
   constexpr int NCW = (K3 + SKF_CW - 1) / SKF_CW;
   __shared__ double red[MAX_R * SKF_NPART * SKF_CW];
@@ -651,6 +1001,46 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
   const int wgx = blockIdx.x;
   Stamp st_{};
   st_.mark(0);
+  if (wgx < n_gene_wg && ybuf) {
+    constexpr int LPX = 64 / K, LY = K * LPX, YU = 16;  // lanes per component, lanes used
+    const int lane = tid & 63, wv = tid >> 6;
+    const int g = wgx * (SKF_NT / 64) + wv;
+    if (g >= P) return;  // (wave-uniform; no barrier in this branch)
+    const double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
+    const long long w0 = (long long)yptr[g] * K, w1 = (long long)yptr[g + 1] * K;
+    const double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * K;
+    const int x = lane < K ? lane : 0;
+    const double th = theta[((size_t)b * P + g) * K + x];
+    const double ad = nth_add ? nth_add[((size_t)b * P + g) * K + x] : 0.0;
+    const int dg = deg[g];
+    double X0 = R == 2 ? sk_gene_sum<6>(xb, prow_ptr, P, g, x, K, 6)
+                       : sk_gene_sum<3 * MAX_R>(xb, prow_ptr, P, g, x, K, 3 * R);
+    double S = 0.0;
+    if (lane < LY) {
+      for (long long wd = w0 + lane; wd < w1; wd += YU * LY) {
+        double v[YU];
+#pragma unroll
+        for (int u = 0; u < YU; ++u) v[u] = yb[wd + (long long)u * LY < w1 ? wd + (long long)u * LY : wd];
+#pragma unroll
+        for (int u = 0; u < YU; ++u)
+          if (wd + (long long)u * LY < w1) S += v[u];
+      }
+    }
+    double* __restrict__ yr = red + wv * 64;
+    yr[lane] = S;
+    wave_lds_sync();
+    if (lane < K) {
+      double Y = yr[lane];
+#pragma unroll
+      for (int j = 1; j < LPX; ++j) Y += yr[lane + j * K];
+      double X = X0 + Y;
+      if (nth_add) X += ad;
+      const size_t o = ((size_t)b * P + g) * K + lane;
+      if constexpr (SUMS) nth_out[o] = X;
+      else theta[o] = th * X / (double)dg;
+    }
+    return;
+  }
   if (wgx < n_gene_wg) {
     const int item = wgx * SKF_NT + tid;
     if (item >= P * K) return;  // no barrier in this branch

@@ -27,10 +27,11 @@ class EMEngine:
     KERNELS = ("pass_a", "pass_b", "fin")   # kernel ids of include/mmsbm.h's timing calls
     # what each id launches, by plan family (plan_info "small_k"): the large-K kernels (0) run
     # pass A, the gene kernel and the update; the small-K plan (1) pass A, pass B and fin; the
-    # fused small-K plan (2) one fused E-step and fin
+    # fused small-K plans (2: three streams, 3: stream 0 with Y entries) one E-step and fin
     LABELS = {0: {"pass_a": 0, "gene": 1, "fin": 2},
               1: {"pass_a": 0, "pass_b": 1, "fin": 2},
-              2: {"fused": 0, "fin": 2}}
+              2: {"fused": 0, "fin": 2},
+              3: {"fused": 0, "fin": 2}}
 
     def __init__(self, K: int, P: int, B: int = 1, R: int = 2, eps: float = 1e-10, device=None):
         if not torch.cuda.is_available():
