@@ -602,15 +602,15 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
 // their theta gathers, V tables, c and M work and their X contractions — do not exist.  At the
 // unit's end: X^0 of its stretches and the workgroup's S partial, as SK_U does for stream 0;
 // sk_fin_kernel then adds each gene's Y entries (Plan::yptr) to its X^0 partial rows.
-// c is computed per sub-batch of 4 chunks (16 observations, one lane each), so only 4 chunks'
-// Z / Z' stay live in registers between phase 1 (Z, Z', d) and phase 2 (c, Y, M).
+// Each chunk runs start to end (Z, Z', d, c in its 16 lanes, Y, M): the block's 32 theta gathers
+// all go out first, as in SK_U, and no chunk's Z / Z' has to stay live until a batched division.
 // ------------------------------------------------------------------------------------------
 template <int K>
 struct SKY {
   using T = SKT<K>;
   // per wave: slots, the block's (u, v) genes, pivot rows, the block's Y entries, one transpose
-  // buffer, d / c words
-  static constexpr int WAVE = T::GUK * T::SLOT + SK_ROWS + T::THL + SK_ROWS + 64 + SK_ROWS;
+  // buffer
+  static constexpr int WAVE = T::GUK * T::SLOT + SK_ROWS + T::THL + SK_ROWS + 64;
   static constexpr int LDS = (T::PSD + NW * WAVE) * 8;
   static_assert(LDS <= 80 * 1024, "two SK_Y workgroups per CU");
   // the unguarded Z' operand reads (rows b < 4 NG of the last slot, columns up to 15) stay inside
@@ -648,7 +648,6 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
   double* THl = wl + GUK * SLOT + SK_ROWS;                 // pivot theta rows [GUK][4 NG]
   int2* YE = reinterpret_cast<int2*>(THl + T::THL);        // the block's Y entries (slot 1, slot 2)
   double* TRl = THl + T::THL + SK_ROWS;                    // the Z / Z' operand transpose
-  double* DL = TRl + 64;                                   // d, then c, per observation
   double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * K;
   double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
   Stamp st_{};
@@ -782,96 +781,68 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
         stage_block(bk);
         wave_lds_sync();
       }
-      if (nb > LC) load_block(b0 / LC + 1, bk);
-      // ---- theta gathers straight into the MFMA operand registers (lane (obs hi, col): theta_j
-      // and theta_k of its observation, column col; col >= K a finite copy of column K - 1, masked
-      // where a product needs it), one sub-batch of 4 chunks ahead: two windows of 4 chunks live
-      // (the whole block's 32 values would spill)
-      const int2* __restrict__ recb = rec;
-      auto gather = [&](int q0, double (&ga)[4], double (&gv)[4]) {
+      if (nb > LC) load_block(b0 / LC + 1, bk);  // the next block's records, in flight meanwhile
+      // ---- theta gathers: every value of the block at once, straight into the registers of the
+      // MFMA operands (lane (obs hi, col): theta_j and theta_k of its observation, column col;
+      // col >= K a finite copy of column K - 1, masked where a product needs it)
+      double ga[LC], gv[LC];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          ga[u] = 0.0;
-          gv[u] = 0.0;
-          if (q0 + u < nb) {  // (uniform)
-            const int2 rh = recb[(q0 + u) * 4 + hi];
-            const char* __restrict__ thb = reinterpret_cast<const char*>(th);
-            ga[u] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
-            gv[u] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
-          }
+      for (int i = 0; i < LC; ++i) {
+        ga[i] = 0.0;
+        gv[i] = 0.0;
+        if (i < nb) {  // (uniform)
+          const int2 rh = rec[i * 4 + hi];
+          const char* __restrict__ thb = reinterpret_cast<const char*>(th);
+          ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
+          gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
         }
-      };
-      double gaw[2][4], gvw[2][4];
-      gather(0, gaw[0], gvw[0]);
+      }
+      // ---- per chunk: Z and Z' on MFMA (A = the transposed theta_k / theta_j tile through the
+      // wave's LDS, bank-swizzled; theta_j zeroed past K), d by a DPP row sum, c = n / d in the 16
+      // lanes of each observation, the Y entries c Z (gene j) and c Z' (gene k), M += c theta_j (x)
+      // theta_k (k = observation); a finished stretch's M row replaces its V table in slot t
 #pragma unroll
-      for (int sb = 0; sb < LC / 4; ++sb) {
-        if (4 * sb < nb) {  // (uniform)
-          if (sb + 1 < LC / 4 && 4 * (sb + 1) < nb) gather(4 * (sb + 1), gaw[(sb + 1) & 1], gvw[(sb + 1) & 1]);
-          const double(&ga)[4] = gaw[sb & 1];
-          const double(&gv)[4] = gvw[sb & 1];
-          // ---- phase 1, 4 chunks: Z, Z' on MFMA (A = the transposed theta_k / theta_j tile through
-          // the wave's LDS, bank-swizzled; theta_j zeroed past K), d parked one word per observation
-          double zq[4], zpq[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int q = 4 * sb + u;
-            zq[u] = 0.0;
-            zpq[u] = 0.0;
-            if (q < nb) {
-              TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = gv[u];
-              wave_lds_sync();
-              double z = 0.0;
-#pragma unroll
-              for (int hs = 0; hs < NG; ++hs)
-                z = mfma4(TRl[16 * lo + ((4 * hs + hi) ^ (4 * (lo >> 1)))], vb[hs], z);
-              // (a wave's LDS accesses execute in order: the reads above precede this write)
-              TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = kcol ? ga[u] : 0.0;
-              wave_lds_sync();
-              double zp = 0.0;
-#pragma unroll
-              for (int bs = 0; bs < NG; ++bs)
-                zp = mfma4(TRl[16 * lo + ((4 * bs + hi) ^ (4 * (lo >> 1)))], vbt[bs], zp);
-              zq[u] = z;
-              zpq[u] = zp;
-              DL[q * 4 + hi] = row16_sum(ga[u] * z) + eps;
-              if (b0 + q + 1 == vsend) {  // the next stretch's V operands
-                ++vt;
-                vsend = stretch_end(vt);
-                if (vt < nst) load_v(vt);
-              }
-            }
-          }
+      for (int q = 0; q < LC; ++q) {
+        if (q < nb) {
+          TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = gv[q];
           wave_lds_sync();
-          // ---- c = n / d of the sub-batch's 16 observations (lanes 16 sb .. 16 sb + 15)
-          {
-            const double cl = sk_div((double)wlane, DL[lane]);
-            if ((lane >> 4) == sb) DL[lane] = cl;
-          }
+          double z = 0.0;
+#pragma unroll
+          for (int hs = 0; hs < NG; ++hs)
+            z = mfma4(TRl[16 * lo + ((4 * hs + hi) ^ (4 * (lo >> 1)))], vb[hs], z);
+          // (a wave's LDS accesses execute in order: the reads above precede this write)
+          TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = kcol ? ga[q] : 0.0;
           wave_lds_sync();
-          // ---- phase 2: the Y entries c Z (gene j) and c Z' (gene k), M += c theta_j (x) theta_k
-          // (k = observation); a finished stretch's M row replaces its V table in slot t
+          double zp = 0.0;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int q = 4 * sb + u;
-            if (q < nb) {
-              const double c = DL[q * 4 + hi];
-              const int2 ey = YE[q * 4 + hi];
-              if (kcol) {
-                yb[(size_t)ey.x * K + col] = c * zq[u];
-                yb[(size_t)ey.y * K + col] = c * zpq[u];
-              }
-              m16 = mfma16(ga[u], c * gv[u], m16);
-              if (b0 + q + 1 == send) {
+          for (int bs = 0; bs < NG; ++bs)
+            zp = mfma4(TRl[16 * lo + ((4 * bs + hi) ^ (4 * (lo >> 1)))], vbt[bs], zp);
+          // the count of observation hi of this chunk (lane 4 q + hi's record), by scalar reads
+          const int n0 = __builtin_amdgcn_readlane(wlane, 4 * q), n1 = __builtin_amdgcn_readlane(wlane, 4 * q + 1);
+          const int n2 = __builtin_amdgcn_readlane(wlane, 4 * q + 2), n3 = __builtin_amdgcn_readlane(wlane, 4 * q + 3);
+          const int nq = hi == 0 ? n0 : hi == 1 ? n1 : hi == 2 ? n2 : n3;
+          const double d = row16_sum(ga[q] * z) + eps;
+          const double c = sk_div((double)nq, d);
+          const int2 ey = YE[q * 4 + hi];
+          if (kcol) {
+            yb[(size_t)ey.x * K + col] = c * z;
+            yb[(size_t)ey.y * K + col] = c * zp;
+          }
+          m16 = mfma16(ga[q], c * gv[q], m16);
+          if (b0 + q + 1 == vsend) {  // the next stretch's V operands
+            ++vt;
+            vsend = stretch_end(vt);
+            if (vt < nst) load_v(vt);
+          }
+          if (b0 + q + 1 == send) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                  const int x = hi + 4 * i;
-                  if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
-                }
-                m16 = d4v{0.0, 0.0, 0.0, 0.0};
-                ++t;
-                send = stretch_end(t);
-              }
+            for (int i = 0; i < 4; ++i) {
+              const int x = hi + 4 * i;
+              if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[i];
             }
+            m16 = d4v{0.0, 0.0, 0.0, 0.0};
+            ++t;
+            send = stretch_end(t);
           }
         }
       }
@@ -1013,11 +984,20 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
     const double th = theta[((size_t)b * P + g) * K + x];
     const double ad = nth_add ? nth_add[((size_t)b * P + g) * K + x] : 0.0;
     const int dg = deg[g];
+    // the first round of Y loads is in flight before the X^0 partial rows' dependent loads (at
+    // fold0 most genes need one round: ~96 entries of K words over LY lanes)
+    const long long wf = w0 + (lane < LY ? lane : 0);
+    double v0[YU];
+#pragma unroll
+    for (int u = 0; u < YU; ++u) v0[u] = yb[wf + (long long)u * LY < w1 ? wf + (long long)u * LY : wf];
     double X0 = R == 2 ? sk_gene_sum<6>(xb, prow_ptr, P, g, x, K, 6)
                        : sk_gene_sum<3 * MAX_R>(xb, prow_ptr, P, g, x, K, 3 * R);
     double S = 0.0;
     if (lane < LY) {
-      for (long long wd = w0 + lane; wd < w1; wd += YU * LY) {
+#pragma unroll
+      for (int u = 0; u < YU; ++u)
+        if (wf + (long long)u * LY < w1) S += v0[u];
+      for (long long wd = wf + YU * LY; wd < w1; wd += YU * LY) {
         double v[YU];
 #pragma unroll
         for (int u = 0; u < YU; ++u) v[u] = yb[wd + (long long)u * LY < w1 ? wd + (long long)u * LY : wd];
