@@ -706,10 +706,32 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
   load_block(0, bk);
   Unit un;
   load_unit(un);
+  // the first block's theta gathers go out as soon as its records are in the wave's LDS, before
+  // P^0 is staged and the V tables are formed: a unit is only a few chunks long, so the gathers'
+  // latency would otherwise sit on the wave's path once per unit
+  stage_block(bk);
+  wave_lds_sync();
+  const int colc = col < K ? col : K - 1;
+  const unsigned cb = (unsigned)colc * 8u;
+  const bool kcol = col < K;
+  double ga[LC], gv[LC];
+  auto gather = [&](int nb) {
+#pragma unroll
+    for (int i = 0; i < LC; ++i) {
+      ga[i] = 0.0;
+      gv[i] = 0.0;
+      if (i < nb) {  // (uniform)
+        const int2 rh = REC[i * 4 + hi];
+        const char* __restrict__ thb = reinterpret_cast<const char*>(th);
+        ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
+        gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
+      }
+    }
+  };
+  gather(un.nst > 0 ? (un.c1 < LC ? un.c1 : LC) : 0);
 #pragma unroll
   for (int i = 0; i < T::NPV; ++i)
     if (tid + NT * i < T::PSD) PV[tid + NT * i] = pvv[i];
-  stage_block(bk);
   __syncthreads();  // P^0_r published (the V tables below read it)
   st_.mark(6);
 
@@ -726,10 +748,6 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
         if (t + 1 == i && i < nst) e = ds[i];
       return e;
     };
-    const int2* __restrict__ rec = REC;
-    const int colc = col < K ? col : K - 1;
-    const unsigned cb = (unsigned)colc * 8u;
-    const bool kcol = col < K;
     const auto& tv = un.tv;
     // ---- V_g[cell] = sum_a theta_g[a] P^0[a][cell] for the unit's genes into their slots (every
     // word of the GUK slots written: zero past K^2 and for absent stretches); pivot theta rows to
@@ -776,27 +794,17 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
     load_v(0);
     for (int b0 = 0; b0 < c1; b0 += LC) {
       const int nb = c1 - b0;
+      // ---- theta gathers: every value of the block at once, straight into the registers of the
+      // MFMA operands (lane (obs hi, col): theta_j and theta_k of its observation, column col;
+      // col >= K a finite copy of column K - 1, masked where a product needs it); the first
+      // block's went out in the prologue
       if (b0 > 0) {
         wave_lds_sync();
         stage_block(bk);
         wave_lds_sync();
+        gather(nb);
       }
       if (nb > LC) load_block(b0 / LC + 1, bk);  // the next block's records, in flight meanwhile
-      // ---- theta gathers: every value of the block at once, straight into the registers of the
-      // MFMA operands (lane (obs hi, col): theta_j and theta_k of its observation, column col;
-      // col >= K a finite copy of column K - 1, masked where a product needs it)
-      double ga[LC], gv[LC];
-#pragma unroll
-      for (int i = 0; i < LC; ++i) {
-        ga[i] = 0.0;
-        gv[i] = 0.0;
-        if (i < nb) {  // (uniform)
-          const int2 rh = rec[i * 4 + hi];
-          const char* __restrict__ thb = reinterpret_cast<const char*>(th);
-          ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
-          gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
-        }
-      }
       // ---- per chunk: Z and Z' on MFMA (A = the transposed theta_k / theta_j tile through the
       // wave's LDS, bank-swizzled; theta_j zeroed past K), d by a DPP row sum, c = n / d in the 16
       // lanes of each observation, the Y entries c Z (gene j) and c Z' (gene k), M += c theta_j (x)
