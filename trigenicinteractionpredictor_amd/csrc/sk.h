@@ -41,6 +41,9 @@ enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
 #ifndef MMSBM_SK_MRED
 #define MMSBM_SK_MRED 0  // 1: d's sum over b on MFMA, four chunks at a time (measured slower than the DPP row sum)
 #endif
+#ifndef MMSBM_SK_GHOIST
+#define MMSBM_SK_GHOIST 0  // 1: the first block's theta gathers before the V tables (after the barrier)
+#endif
 
 constexpr int LC = mmsbm_plan::SK_BLOCK;          // chunks of one block (gathered at once)
 constexpr int SK_ROWS = 4 * mmsbm_plan::SK_BLOCK;  // records staged per wave (one block, one per lane)
@@ -257,6 +260,27 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     const unsigned cb = (unsigned)colc * 8u;
     const bool kcol = col < K;
     const auto& tv = un.tv;  // (array references: the indices stay compile-time constants)
+    // ---- theta gathers: every value of a block at once, straight into the registers of the
+    // MFMA operands (lane (obs hi, col): theta_u and theta_v of its observation, column col);
+    // columns col >= K are zeroed where a product needs it (the Z operand and d), at first use,
+    // so no select waits for a load here
+    double ga[LC], gv[LC];
+    auto gather = [&](int nb) {
+#pragma unroll
+      for (int i = 0; i < LC; ++i) {
+        ga[i] = 0.0;  // (chunks past the unit's end stay zero)
+        gv[i] = 0.0;
+        if (i < nb) {  // uniform guard: a short block issues only its own loads
+          const int2 rh = rec[i * 4 + hi];  // (u gene, v gene): make_slots orders them
+          // (32-bit byte offsets from the sample's theta base: one 24-bit multiply-add per address;
+          // col >= K reads a finite copy of column K - 1)
+          const char* __restrict__ thb = reinterpret_cast<const char*>(th);
+          ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
+          gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
+        }
+      }
+    };
+    if constexpr (MMSBM_SK_GHOIST) gather(c1 < LC ? c1 : LC);  // (in flight during the V tables)
     if constexpr (MODE != SK_B) {
       // ---- V_g[cell] = sum_a theta_g[a] P^s[a][cell] for the unit's genes (m = gene, k = a, B
       // from the staged lattice: rows a >= K meet zero theta, words past K^3 are zero), into slot g
@@ -317,24 +341,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
         wave_lds_sync();
       }
       if (nb > LC) load_block(b0 / LC + 1, bk);  // the next block's records, in flight meanwhile
-      // ---- theta gathers: every value of the block at once, straight into the registers of the
-      // MFMA operands (lane (obs hi, col): theta_u and theta_v of its observation, column col);
-      // columns col >= K are zeroed where a product needs it (the Z operand and d), at first use,
-      // so no select waits for a load here
-      double ga[LC], gv[LC];
-#pragma unroll
-      for (int i = 0; i < LC; ++i) {
-        ga[i] = 0.0;  // (chunks past the unit's end stay zero)
-        gv[i] = 0.0;
-        if (i < nb) {  // uniform guard: a short block issues only its own loads
-          const int2 rh = rec[i * 4 + hi];  // (u gene, v gene): make_slots orders them
-          // (32-bit byte offsets from the sample's theta base: one 24-bit multiply-add per address;
-          // col >= K reads a finite copy of column K - 1)
-          const char* __restrict__ thb = reinterpret_cast<const char*>(th);
-          ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
-          gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
-        }
-      }
+      if (!MMSBM_SK_GHOIST || b0 > 0) gather(nb);
       if constexpr (MODE != SK_B) {
         // ---- d of every observation of the block.  Per chunk: Z[obs hi][b = col] =
         // sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA (A = theta_v(obs lo)[4 hs + hi], the transpose
