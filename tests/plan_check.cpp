@@ -25,7 +25,9 @@ static int fail(const char* what, long long a = 0, long long b = 0) {
 // slot 1 / 2) whose slot gene is g, and padding rows name the dummy entry n_y
 static int check_y(const Plan& pl, int P, long long n_obs) {
 
-  if (pl.n_y != 2 * n_obs || (int)pl.yptr.size() != P + 1 || pl.yptr[0] != 0 || pl.yptr[P] != pl.n_y)
+  const bool py = !pl.prow_y.empty();  // SK_Y: the partial rows are Y entries too
+  if (pl.n_y != 2 * n_obs + (py ? pl.n_prows : 0) || (int)pl.yptr.size() != P + 1 || pl.yptr[0] != 0 ||
+      pl.yptr[P] != pl.n_y)
     return fail("yptr", pl.n_y, 2 * n_obs);
   if ((long long)pl.row_y.size() != 2 * pl.n_rows0) return fail("row_y size");
   {
@@ -46,6 +48,11 @@ static int check_y(const Plan& pl, int P, long long n_obs) {
         if (owner[e] != (k == 0 ? x.y : x.z)) return fail("row_y gene", q, e);
         hits[e]++;
       }
+    }
+    for (long long q = 0; py && q < pl.n_prows; ++q) {
+      const int e = pl.prow_y[q];
+      if (e < 0 || e >= pl.n_y || owner[e] != pl.prow_gene[q]) return fail("prow_y gene", q, e);
+      hits[e]++;
     }
     for (long long e = 0; e < pl.n_y; ++e)
       if (hits[e] != 1) return fail("y entry coverage", e, hits[e]);
@@ -159,6 +166,8 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
       if (d[D_NST] == 0) continue;
       const int u = pl.wg_ustart[(int)(slot / per)] + (int)(slot % per);
       const int* du = &pl.udesc[(size_t)u * UD];
+      for (int t = 0; t < d[D_NST]; ++t)
+        if (d[D_PROW + t] != pl.prow_y[du[D_PROW + t]]) return fail("SK_Y stretch entry", slot, t);
       for (int i = 0; i < 4 * d[D_END]; ++i)
         for (int k = 0; k < 2; ++k)
           if (pl.sk_urow12[((size_t)slot * 4 * L + i) * 2 + k] != pl.row_y[(4LL * du[0] + i) * 2 + k])

@@ -627,7 +627,12 @@ struct FT {
   static constexpr int NGW = 4 * GT;            // genes per workgroup
   static constexpr int NT = 512;
   static constexpr int KSPLIT = 8 / NXG;        // k-step parts over the 8 waves
-  static constexpr int MS = NGW * K2P + KSPLIT * NGW * KP;  // doubles: summed rows + X parts
+  // LDS row stride of the summed rows: = 20 mod 32 doubles, so the 8 (row lo, k = hi) addresses a
+  // ds_read_b64 lane group reads in x0_tiles fall on distinct banks (K2P = 400 at K = 20 put rows
+  // lo and lo + 2 on the same banks: 58 % of the gene kernel's LDS cycles were conflicts,
+  // profiles/r04d_k20_b8_pmc_summary.txt)
+  static constexpr int MSR = K2P + (20 - K2P % 32 + 32) % 32;
+  static constexpr int MS = NGW * MSR + KSPLIT * NGW * KP;  // doubles: summed rows + X parts
   static constexpr int LDS_SP = 64 * KP;                    // s_partial's theta staging
   static constexpr int LDS = (MS > LDS_SP ? MS : LDS_SP) * 8;
   // LDS that lets two workgroups share a CU (K = 20-23): rounds of 6 partial-row entries and a
@@ -643,7 +648,7 @@ struct FT {
 };
 
 // X0 contraction of GT gene tiles at once: each p load feeds GT MFMAs, over the k-steps [kb, ke).
-// Mg = tile 0's row of lane lo; tile t's row is Mg + 4 t K2P.  p[a][k] = p_r[a K2 + k]; addresses
+// Mg = tile 0's row of lane lo; tile t's row is Mg + 4 t MSR.  p[a][k] = p_r[a K2 + k]; addresses
 // clamped (k >= K2: M is zero there; a >= K: the column is never stored), so every load is
 // unconditional and a round's loads go out together.
 template <int K>
@@ -668,7 +673,7 @@ __device__ __forceinline__ void x0_tiles(const double* __restrict__ Mg, const do
       const bool ok = ks0 + u < ke;
 #pragma unroll
       for (int t = 0; t < GT; ++t) {
-        const double m = Mg[t * 4 * F::K2P + kk[u]];
+        const double m = Mg[t * 4 * F::MSR + kk[u]];
         acc[t] = mfma4(ok ? m : 0.0, bv[u], acc[t]);
       }
     }
@@ -690,7 +695,7 @@ __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const do
   const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
   const int g0 = blockIdx.x * NGW;
   const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
-  double* Xr = Ms + NGW * F::K2P;  // [KSPLIT][NGW][KP]
+  double* Xr = Ms + NGW * F::MSR;  // [KSPLIT][NGW][KP]
   __shared__ int pp[MAX_R][NGW + 1];
   {
     const int c = tid / (NGW + 1), i = tid % (NGW + 1);
@@ -735,7 +740,7 @@ __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const do
       double m = qa < qb ? v1[u] : 0.0;
       if (qa + 1 < qb) m += v2[u];
       for (int q = qa + 2; q < qb; ++q) m += pb[(size_t)q * K2 + kk];
-      if (idx < NE) Ms[idx] = m;
+      if (idx < NE) Ms[(idx / F::K2P) * F::MSR + idx % F::K2P] = m;
     }
   };
   __syncthreads();  // pp
@@ -759,7 +764,7 @@ __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const do
     st_.mark(1);
     if (nxt < R) load_round(nxt, tid);
     const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-    x0_tiles<K>(Ms + (size_t)lo * F::K2P, p, a, hi, kb, ke, acc);
+    x0_tiles<K>(Ms + (size_t)lo * F::MSR, p, a, hi, kb, ke, acc);
     r = nxt;
   }
   st_.mark(2);
@@ -1155,8 +1160,8 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
     L.cbuf = off;
     off += align_up(c->sk_y ? B * (tr.n_y + 1) * c->K * 8
                             : B * std::max<long long>(tr.sk_slots[1] * 4 * tr.sk_L[1], 1) * 8);
-    L.prows = off;
-    off += align_up(B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
+    L.prows = off;  // (SK_Y: the X rows are Y entries)
+    off += align_up(c->sk_y ? 8 : B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
     L.spart = off;
     off += align_up(B * std::max(tr.n_wg_a, 1) * K3 * 8);
     L.gx = off;

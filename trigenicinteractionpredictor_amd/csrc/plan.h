@@ -78,7 +78,8 @@ struct Plan {
   // large-K EM plans only: Y entries (see the header)
   std::vector<int> row_y;          // [n_rows0][2] slot-1 / slot-2 entry of each stream-0 row
   std::vector<int> yptr;           // [P + 1] entries of each gene
-  long long n_y = 0;               // 2 x observations
+  long long n_y = 0;               // 2 x observations (+ the partial rows of a small-K SK_Y plan)
+  std::vector<int> prow_y;         // small-K SK_Y plans: the Y entry of each (stream-0) partial row
   int rounds_a = 1, rounds_b = 1;  // unit rounds per workgroup (stream 0 / streams 1, 2)
   long long n_units = 0;
   // slot layout the small-K kernels read (make_slots below); group 0 = stream 0 (pass A), group 1 =
@@ -176,6 +177,8 @@ inline void make_slots(Plan& pl) {
         const int c0 = d[0];
         for (int t = 0; t < UD; ++t) sd[t] = d[t];
         for (int t = 0; t <= D_END; ++t) sd[t] = d[t] - c0;
+        if (!pl.prow_y.empty())  // SK_Y: a stretch's X^0 row goes to its Y entry
+          for (int t = 0; t < d[D_NST]; ++t) sd[D_PROW + t] = pl.prow_y[(size_t)d[D_PROW + t]];
         I4* rec = &pl.sk_urec[g][(size_t)slot * 4 * L];
         const long long row0 = 4LL * c0, nrow = 4LL * (d[D_END] - c0);
         for (long long i = 0; i < 4LL * L; ++i) {
@@ -483,6 +486,10 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
     for (int s = 1; s <= 2; ++s)
       for (int r = 0; r < R; ++r)
         for (int e : obs[r]) pl.yptr[(size_t)ids[(size_t)e * 3 + s] + 1]++;
+    // small-K SK_Y plans: a gene's X^0 partial rows (K words each, written by the pass at its
+    // stretch ends) follow its observation entries, rating then row order, so fin sums one range
+    if (small)
+      for (long long q = 0; q < pl.n_prows; ++q) pl.yptr[(size_t)pl.prow_gene[q] + 1]++;
     for (int g = 0; g < P; ++g) pl.yptr[g + 1] += pl.yptr[g];
     pl.n_y = pl.yptr[P];
     std::vector<int> pos(pl.yptr.begin(), pl.yptr.end() - 1);
@@ -490,6 +497,14 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
     for (int s = 1; s <= 2; ++s)
       for (int r = 0; r < R; ++r)
         for (int e : obs[r]) pl.row_y[(size_t)2 * row0[r][e] + (s - 1)] = pos[ids[(size_t)e * 3 + s]]++;
+    if (small) {
+      pl.prow_y.assign((size_t)pl.n_prows, -1);
+      for (int r = 0; r < R; ++r)
+        for (int g = 0; g < P; ++g) {
+          const int* ptr = &pl.prow_ptr[(size_t)r * (P + 1)];
+          for (int q = ptr[g]; q < ptr[g + 1]; ++q) pl.prow_y[q] = pos[g]++;
+        }
+    }
   }
   for (auto& rec : pl.rows)
     if (rec.w == -2) rec.w = (int)pl.n_rows0;  // padding rows of streams 1, 2: the zero c slot

@@ -607,8 +607,9 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
 // column-wise from its slot), d = eps + th_j . Z, c = n / d, writes the Y entries c Z (gene j)
 // and c Z' (gene k) and accumulates M^0 += c th_j (x) th_k.  Streams 1 and 2 — their records,
 // their theta gathers, V tables, c and M work and their X contractions — do not exist.  At the
-// unit's end: X^0 of its stretches and the workgroup's S partial, as SK_U does for stream 0;
-// sk_fin_kernel then adds each gene's Y entries (Plan::yptr) to its X^0 partial rows.
+// unit's end: X^0 of its stretches (into the stretch's own Y entry, Plan::prow_y) and the
+// workgroup's S partial, as SK_U does for stream 0; sk_fin_kernel then sums each gene's Y range
+// (Plan::yptr: its observation entries, then its X^0 rows) in one pass.
 // Each chunk runs start to end (Z, Z', d, c in its 16 lanes, Y, M): the block's 32 theta gathers
 // all go out first, as in SK_U, and no chunk's Z / Z' has to stay live until a batched division.
 // ------------------------------------------------------------------------------------------
@@ -656,7 +657,8 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
   int2* YE = reinterpret_cast<int2*>(THl + T::THL);        // the block's Y entries (slot 1, slot 2)
   double* TRl = THl + T::THL + SK_ROWS;                    // the Z / Z' operand transpose
   double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * K;
-  double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
+  (void)xpart;
+  (void)n_prows;
   Stamp st_{};
   st_.mark(0);
 
@@ -874,7 +876,8 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
         for (int ks = 0; ks < NCT; ++ks)
           xa[ks & 3] = mfma4(MSl[(4 * tt + lo) * SLOT + 4 * ks + hi], pz[4 * ks], xa[ks & 3]);
         const double xacc = (xa[0] + xa[1]) + (xa[2] + xa[3]);
-        if (4 * tt + hi < nst && blk < NG && z < K) xb[(size_t)un.prow[tt] * K + z] = xacc;
+        // (the stretch's Y entry: fin sums it with the gene's observation entries)
+        if (4 * tt + hi < nst && blk < NG && z < K) yb[(size_t)un.prow[tt] * K + z] = xacc;
       }
     }
     st_.mark(3);
@@ -992,21 +995,18 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
     const int lane = tid & 63, wv = tid >> 6;
     const int g = wgx * (SKF_NT / 64) + wv;
     if (g >= P) return;  // (wave-uniform; no barrier in this branch)
-    const double* __restrict__ xb = xpart + (size_t)b * n_prows * K;
     const long long w0 = (long long)yptr[g] * K, w1 = (long long)yptr[g + 1] * K;
     const double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * K;
     const int x = lane < K ? lane : 0;
     const double th = theta[((size_t)b * P + g) * K + x];
     const double ad = nth_add ? nth_add[((size_t)b * P + g) * K + x] : 0.0;
     const int dg = deg[g];
-    // the first round of Y loads is in flight before the X^0 partial rows' dependent loads (at
-    // fold0 most genes need one round: ~96 entries of K words over LY lanes)
+    // the gene's Y range holds its observation entries and its X^0 partial rows (at fold0 ~100
+    // entries of K words: one round of YU loads over LY lanes for most genes)
     const long long wf = w0 + (lane < LY ? lane : 0);
     double v0[YU];
 #pragma unroll
     for (int u = 0; u < YU; ++u) v0[u] = yb[wf + (long long)u * LY < w1 ? wf + (long long)u * LY : wf];
-    double X0 = R == 2 ? sk_gene_sum<6>(xb, prow_ptr, P, g, x, K, 6)
-                       : sk_gene_sum<3 * MAX_R>(xb, prow_ptr, P, g, x, K, 3 * R);
     double S = 0.0;
     if (lane < LY) {
 #pragma unroll
@@ -1028,7 +1028,7 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
       double Y = yr[lane];
 #pragma unroll
       for (int j = 1; j < LPX; ++j) Y += yr[lane + j * K];
-      double X = X0 + Y;
+      double X = Y;
       if (nth_add) X += ad;
       const size_t o = ((size_t)b * P + g) * K + lane;
       if constexpr (SUMS) nth_out[o] = X;
