@@ -435,12 +435,14 @@ def test_in_place_link_edit_between_iterations_matches_oracle():
                                    (10, {"MMSBM_SK_FUSED": "0"}), (11, {"MMSBM_SK_FUSED": "0"}),
                                    (9, {"MMSBM_SK_FUSED": "0", "MMSBM_UNITS": "7,3"}),
                                    (10, {"MMSBM_UNITS": "1,1"}), (5, {"MMSBM_UNITS": "40,40"}),
-                                   (10, {"MMSBM_SK_Y": "0"}), (12, {"MMSBM_SK_Y": "0"}),
-                                   (3, {"MMSBM_SK_Y": "0", "MMSBM_UNITS": "7,3"}),
-                                   (1, {}), (2, {}), (4, {"MMSBM_UNITS": "3,3"}), (11, {})])
+                                   (10, {"MMSBM_SK_Y": "1"}), (12, {"MMSBM_SK_Y": "1"}),
+                                   (3, {"MMSBM_SK_Y": "1", "MMSBM_UNITS": "7,3"}),
+                                   (1, {"MMSBM_SK_Y": "1"}), (2, {"MMSBM_SK_Y": "1"}),
+                                   (4, {"MMSBM_SK_Y": "1", "MMSBM_UNITS": "3,3"}),
+                                   (11, {"MMSBM_SK_Y": "1"}), (9, {"MMSBM_SK_Y": "1", "MMSBM_UNITS": "1,1"})])
 def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
-    """K <= 12 runs the small-K kernels (csrc/sk.h; the stream-0 E-step with Y entries by default
-    (SK_Y), the three-stream fused E-step with MMSBM_SK_Y=0, pass A + pass B with
+    """K <= 12 runs the small-K kernels (csrc/sk.h; the three-stream fused E-step by default
+    (SK_U), the stream-0 E-step with Y entries with MMSBM_SK_Y=1 (SK_Y), pass A + pass B with
     MMSBM_SK_FUSED=0; 8 stretches per unit at K <= 10, 4 above), K > 12 the large-K ones;
     MMSBM_SK=0 forces the large-K family at K=10, MMSBM_UNITS forces long (up to 128 chunks: eight
     16-chunk blocks per unit) or short units.  Every variant matches the C oracle (2 iterations,
@@ -456,7 +458,7 @@ def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
     info = m._engine.plan_info()
     small = K <= 12 and env.get("MMSBM_SK") != "0"
     assert info["small_k"] == (0 if not small else 1 if env.get("MMSBM_SK_FUSED") == "0"
-                               else 2 if env.get("MMSBM_SK_Y") == "0" else 3)
+                               else 3 if env.get("MMSBM_SK_Y") == "1" else 2)
     if small:
         assert info["genes_per_wg_max"] == (8 if K <= 10 else 4)
     th_o, pr_o, L_o, LT_o = _oracle_run(m, theta0, pr0, 2)

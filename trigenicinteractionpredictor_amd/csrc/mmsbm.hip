@@ -1107,7 +1107,7 @@ struct mmsbm_ctx {
   int gcap = 0;                  // most pivot genes per stream-0 workgroup (<= KT<K>::GMAX)
   bool sk = false;               // K <= 12: the small-K kernels of sk.h (MMSBM_SK=0: the large-K ones)
   bool sk_fused = false;         // small-K: one fused E-step launch (SK_U) instead of pass A + pass B
-  bool sk_y = false;             // small-K fused: the stream-0 E-step with Y entries (SK_Y, default)
+  bool sk_y = false;             // small-K fused: the stream-0 E-step with Y entries (SK_Y, MMSBM_SK_Y=1)
   SetDev sets[2];
   int* deg = nullptr;            // device, owned
   std::vector<int> deg_host;
@@ -1559,8 +1559,13 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
       c->ws_bytes = 0;
     }
     c->sk_fused = fused;
-    const char* y = getenv("MMSBM_SK_Y");  // SK_Y (default); 0: the three-stream fused E-step (SK_U)
-    const bool sky = fused && !(y && y[0] == '0');
+    // MMSBM_SK_Y=1: the stream-0 E-step with Y entries (SK_Y) instead of the three-stream fused
+    // E-step (SK_U, the default).  Same-box A/B (profiles/r04j_sky_ab.txt): SK_Y does less than half
+    // SK_U's work and wins where the grid is throughput-bound (fold0 K=10, 8 samples: 78.2k vs 62.1k
+    // sample-iter/s) but loses at one sample, where both are bound by one wave's latency chain
+    // (25.1 vs 23.2 us per iteration).  The choice cannot follow B: bits must not depend on the batch.
+    const char* y = getenv("MMSBM_SK_Y");
+    const bool sky = fused && y && y[0] == '1';
     if (sky != c->sk_y) {  // the plans hold different streams: set links again
       DeviceGuard g(c->device);
       for (auto& sd : c->sets) sd.release();
