@@ -174,6 +174,29 @@ static int check_small(const Plan& pl, int R, int P, long long nch) {
             return fail("SK_Y urow12", slot, i);
     }
   } else {
+    // gene-major X partial rows: gptr tiles [0, n_prows), each row's position lies in its gene's
+    // range, ranges follow (stream, rating, row) order, and the slot descriptors name positions
+    if ((int)pl.gptr.size() != P + 1 || pl.gptr[P] != pl.n_prows || (long long)pl.prow_g.size() != pl.n_prows)
+      return fail("gptr", pl.n_prows);
+    std::vector<int> seen(pl.n_prows, 0);
+    for (long long q = 0; q < pl.n_prows; ++q) {
+      const int g = pl.prow_gene[q], e = pl.prow_g[q];
+      if (e < pl.gptr[g] || e >= pl.gptr[g + 1]) return fail("prow_g range", q, e);
+      if (seen[e]++) return fail("prow_g twice", q, e);
+      if (q > 0 && pl.prow_gene[q - 1] == g && pl.prow_g[q - 1] != e - 1) return fail("prow_g order", q, e);
+    }
+    for (int g2 = 0; g2 < 2; ++g2) {
+      const int per = NW * (g2 == 0 ? pl.rounds_a : pl.rounds_b);
+      const int w0 = g2 == 0 ? 0 : pl.n_wg_a;
+      for (long long slot = 0; slot < pl.sk_slots[g2]; ++slot) {
+        const int* d = &pl.sk_udesc[g2][(size_t)slot * UD];
+        if (d[D_NST] == 0) continue;
+        const int u = pl.wg_ustart[w0 + (int)(slot / per)] + (int)(slot % per);
+        const int* du = &pl.udesc[(size_t)u * UD];
+        for (int t = 0; t < d[D_NST]; ++t)
+          if (d[D_PROW + t] != pl.prow_g[du[D_PROW + t]]) return fail("slot prow_g", slot, t);
+      }
+    }
     const int La = pl.sk_L[0], Lb = pl.sk_L[1];
     for (long long i = 0; i < pl.sk_slots[0] * 4 * La; ++i) {
       const I4& a = pl.sk_urec[0][i];

@@ -817,6 +817,12 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
   const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
   Stamp st_{};
   st_.mark(0);
+#ifdef MMSBM_GENE_ONLY  // measurement builds: run one workgroup kind only (1 gene, 2 S, 4 Y)
+  {
+    const int kind = w < n_gene_wg ? 1 : w < n_gene_wg + n_sp_wg ? 2 : 4;
+    if (!(MMSBM_GENE_ONLY & kind)) return;
+  }
+#endif
   if (w < n_gene_wg) {
     genes_x0<K>(pr, prows, prow_ptr, P, R, n_prows, x0, Ms, st_);
   } else if (w < n_gene_wg + n_sp_wg) {
@@ -1068,6 +1074,7 @@ struct SetDev {  // device copy of one link set's plan
   int* sp_desc = nullptr;
   int* row_y = nullptr;                 // large-K EM plans: Y entries of each stream-0 row,
   int* yptr = nullptr;                  // and each gene's entry range
+  int* gptr = nullptr;                  // small-K: each gene's gene-major X partial rows
   int* sku[2] = {nullptr, nullptr};     // small-K plans (sk.h): slot descriptors of each group,
   int4* skr[2] = {nullptr, nullptr};    // slot-major records,
   int* skrow12 = nullptr;               // slot-major row12 of group 0
@@ -1075,7 +1082,7 @@ struct SetDev {  // device copy of one link set's plan
   int unit_target = 0;
   void release() {
     void* ps[] = {rows, chunk_prow, chunk_vslot, wg_units, wg_code, wg_gene, vgenes, prow_ptr, prow_gene, sp_desc,
-                  row_y, yptr, sku[0], sku[1], skr[0], skr[1], skrow12};
+                  row_y, yptr, gptr, sku[0], sku[1], skr[0], skr[1], skrow12};
     for (void* p : ps)
       if (p) (void)hipFree(p);
     *this = SetDev();
@@ -1368,11 +1375,11 @@ int launch_sk_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nt
   const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
   if (sums)
     sk_fin_kernel<K, true><<<dim3(ngw + ncw, c->B), SKF_NT, 0, s>>>(
-        theta, pr, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
+        theta, pr, c->prows, sd.gptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, nullptr, nullptr, 0, yb, sd.yptr, h.n_y);
   else
     sk_fin_kernel<K, false><<<dim3(ngw + ncw + nqc, c->B), SKF_NT, 0, s>>>(
-        theta, pr, c->prows, sd.prow_ptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
+        theta, pr, c->prows, sd.gptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg, yb, sd.yptr,
         h.n_y);
   HIP_TRY(hipGetLastError());
@@ -1655,6 +1662,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   if ((rc = upload(&sd.sp_desc, h.sp_desc))) return rc;
   if ((rc = upload(&sd.row_y, h.row_y))) return rc;
   if ((rc = upload(&sd.yptr, h.yptr))) return rc;
+  if ((rc = upload(&sd.gptr, h.gptr))) return rc;
   for (int g = 0; g < 2; ++g) {
     if ((rc = upload(&sd.sku[g], h.sk_udesc[g]))) return rc;
     if ((rc = upload(&sd.skr[g], h.sk_urec[g]))) return rc;

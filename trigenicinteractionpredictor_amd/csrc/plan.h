@@ -80,6 +80,10 @@ struct Plan {
   std::vector<int> yptr;           // [P + 1] entries of each gene
   long long n_y = 0;               // 2 x observations (+ the partial rows of a small-K SK_Y plan)
   std::vector<int> prow_y;         // small-K SK_Y plans: the Y entry of each (stream-0) partial row
+  // small-K three-stream plans: the X partial rows gene-major (a gene's rows of every (stream,
+  // rating) in one range, (stream, rating, row) order inside: fin sums one range per gene)
+  std::vector<int> prow_g;         // [n_prows] gene-major position of each partial row
+  std::vector<int> gptr;           // [P + 1] each gene's range of gene-major positions
   int rounds_a = 1, rounds_b = 1;  // unit rounds per workgroup (stream 0 / streams 1, 2)
   long long n_units = 0;
   // slot layout the small-K kernels read (make_slots below); group 0 = stream 0 (pass A), group 1 =
@@ -179,6 +183,8 @@ inline void make_slots(Plan& pl) {
         for (int t = 0; t <= D_END; ++t) sd[t] = d[t] - c0;
         if (!pl.prow_y.empty())  // SK_Y: a stretch's X^0 row goes to its Y entry
           for (int t = 0; t < d[D_NST]; ++t) sd[D_PROW + t] = pl.prow_y[(size_t)d[D_PROW + t]];
+        else if (!pl.prow_g.empty())  // a stretch's X row goes to its gene-major position
+          for (int t = 0; t < d[D_NST]; ++t) sd[D_PROW + t] = pl.prow_g[(size_t)d[D_PROW + t]];
         I4* rec = &pl.sk_urec[g][(size_t)slot * 4 * L];
         const long long row0 = 4LL * c0, nrow = 4LL * (d[D_END] - c0);
         for (long long i = 0; i < 4LL * L; ++i) {
@@ -521,6 +527,18 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
         }
     }
     pl.n_sp = pl.n_wg_a;
+    if (em && !ymode) {  // gene-major X partial rows
+      pl.gptr.assign((size_t)P + 1, 0);
+      for (long long q = 0; q < pl.n_prows; ++q) pl.gptr[(size_t)pl.prow_gene[q] + 1]++;
+      for (int g = 0; g < P; ++g) pl.gptr[g + 1] += pl.gptr[g];
+      std::vector<int> at(pl.gptr.begin(), pl.gptr.end() - 1);
+      pl.prow_g.assign((size_t)pl.n_prows, -1);
+      for (int c = 0; c < 3 * R; ++c)
+        for (int g = 0; g < P; ++g) {
+          const int* ptr = &pl.prow_ptr[(size_t)c * (P + 1)];
+          for (int q = ptr[g]; q < ptr[g + 1]; ++q) pl.prow_g[q] = at[g]++;
+        }
+    }
     make_slots(pl);
     return pl;
   }

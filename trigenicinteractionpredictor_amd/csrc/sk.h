@@ -927,9 +927,8 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
 
 // ------------------------------------------------------------------------------------------
 // sk_fin_kernel, grid (gene workgroups + cell workgroups + q workgroups, B), block 256.
-//   gene part: thread (g, x): X = sum over the 3 R (stream, rating) combos of g's X partials, in
-//     combo then row order (+ the joint model's pair sums); theta' = theta X / deg (:1016-1018)
-//     or, SUMS, nth = X.  SK_Y plans (ybuf set): one wave per gene; its Y entries (one contiguous
+//   gene part: thread (g, x): X = the sum of g's X partials (gene-major: (stream, rating, row)
+//     order) (+ the joint model's pair sums); theta' = theta X / deg (:1016-1018) or, SUMS, nth = X.  SK_Y plans (ybuf set): one wave per gene; its Y entries (one contiguous
 //     block of K-word rows, Plan::yptr) are summed by lanes l < K floor(64 / K), lane l taking
 //     words l, l + LY, ... (component l mod K), the lanes of one component then added in lane
 //     order; lane x < K adds that to its X^0 partial rows (stream 0) and updates theta.
@@ -940,37 +939,20 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
 // ------------------------------------------------------------------------------------------
 constexpr int SKF_NT = 256, SKF_CW = 16, SKF_NPART = 16;
 
-// sum of gene g's X partials (component x) over the combos c < nc, combo then row order; the
-// first row of every combo is loaded with all of them in flight
-template <int NCC>
-__device__ __forceinline__ double sk_gene_sum(const double* __restrict__ xb, const int* __restrict__ prow_ptr,
-                                              int P, int g, int x, int K, int nc) {
-  int qa[NCC], qb[NCC];
-#pragma unroll
-  for (int c = 0; c < NCC; ++c) {
-    const int cc = c < nc ? c : 0;
-    qa[c] = prow_ptr[(size_t)cc * (P + 1) + g];
-    qb[c] = prow_ptr[(size_t)cc * (P + 1) + g + 1];
-  }
-  double v1[NCC];
-#pragma unroll
-  for (int c = 0; c < NCC; ++c) v1[c] = xb[(size_t)(qa[c] < qb[c] ? qa[c] : 0) * K + x];
+// sum of gene g's X partials (component x): its gene-major range [gptr[g], gptr[g + 1]) of
+// partial rows ((stream, rating, row) order, Plan::prow_g), 8 loads in flight (a hub gene's pivot
+// runs span many units); one dependent round for the range, then the rows
+__device__ __forceinline__ double sk_gene_sum(const double* __restrict__ xb, const int* __restrict__ gptr,
+                                              int g, int x, int K) {
+  const int q0 = gptr[g], q1 = gptr[g + 1];
   double X = 0.0;
+  for (int q = q0; q < q1; q += 8) {
+    double v[8];
 #pragma unroll
-  for (int c = 0; c < NCC; ++c) {
-    if (c < nc && qa[c] < qb[c]) {
-      X += v1[c];
-      // the rest of the combo's rows 8 loads at a time (a hub gene's pivot runs span many units),
-      // added in row order
-      for (int q = qa[c] + 1; q < qb[c]; q += 8) {
-        double v[8];
+    for (int u = 0; u < 8; ++u) v[u] = xb[(size_t)(q + u < q1 ? q + u : q) * K + x];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = xb[(size_t)(q + u < qb[c] ? q + u : q) * K + x];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (q + u < qb[c]) X += v[u];
-      }
-    }
+    for (int u = 0; u < 8; ++u)
+      if (q + u < q1) X += v[u];
   }
   return X;
 }
@@ -978,7 +960,7 @@ __device__ __forceinline__ double sk_gene_sum(const double* __restrict__ xb, con
 template <int K, bool SUMS>
 __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
     double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ xpart,
-    const int* __restrict__ prow_ptr, const double* __restrict__ spart, const int* __restrict__ deg,
+    const int* __restrict__ gptr, const double* __restrict__ spart, const int* __restrict__ deg,
     SpRange spr, int P, int R, long long n_prows, int n_wg_a, int n_gene_wg, double eps,
     double* __restrict__ nth_out, double* __restrict__ S_out, const double* __restrict__ nth_add,
     const double* __restrict__ q_part, double* __restrict__ q_out, int n_qwg,
@@ -1044,8 +1026,7 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
     const double th = theta[((size_t)b * P + g) * K + x];
     const double ad = nth_add ? nth_add[((size_t)b * P + g) * K + x] : 0.0;
     const int dg = deg[g];
-    double X = R == 2 ? sk_gene_sum<6>(xb, prow_ptr, P, g, x, K, 6)
-                      : sk_gene_sum<3 * MAX_R>(xb, prow_ptr, P, g, x, K, 3 * R);
+    double X = sk_gene_sum(xb, gptr, g, x, K);
     if (nth_add) X += ad;
     const size_t o = ((size_t)b * P + g) * K + x;
     if constexpr (SUMS) nth_out[o] = X;
