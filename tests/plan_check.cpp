@@ -237,10 +237,13 @@ int main() {
   // (K 11-12), -3 = 8 (K <= 10); fill-packed (the fused launch) -1 = 8, -2 = 4; -4 = fill-packed
   // stream-0 plans with Y entries (SK_Y), 8 stretches
   const bool small = gcap <= 0, fill = gcap == -1 || gcap == -2 || gcap == -4, yent = gcap == -4;
+  // PLAN_NO_BALANCE=1: the large-K units packed whole-run-wise (round 3, MMSBM_BALANCE=0)
+  const bool balance = !getenv("PLAN_NO_BALANCE");
   const int gu = (gcap == 0 || gcap == -2) ? 4 : 8;
   const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill, gu,
                                 85, yent)
-                        : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows);
+                        : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows, false, 1024,
+                                false, GU, 85, false, balance);
   if (fill) {  // every unit but the last of its (stream, rating) section is full: LCAP_SK chunks or GU stretches
     for (long long u = 0; u + 1 < pl.n_units; ++u) {
       const int* d = &pl.udesc[(size_t)u * UD];
@@ -297,12 +300,17 @@ int main() {
   for (int w = 0; w < n_wg; ++w) {
     const int s = pl.wg_code[w] >> 4;
     if ((w < pl.n_wg_a) != (s == 0)) return fail("stream order", w, s);
+    int umin = 1 << 30, umax = 0;
     for (int u = 0; u < NW; ++u) {
       const int c0 = pl.wg_units[w * (NW + 1) + u], c1 = pl.wg_units[w * (NW + 1) + u + 1];
       if (c1 < c0) return fail("unit bounds", w, u);
       if (c1 - c0 > 64) return fail("unit over 64 chunks", w, c1 - c0);
+      umin = std::min(umin, c1 - c0);
+      umax = std::max(umax, c1 - c0);
       for (int c = c0; c < c1; ++c) covered[c]++;
     }
+    // balanced packing: a workgroup's NW units differ by at most one chunk
+    if (balance && umax - umin > 1) return fail("unbalanced units", w, umax - umin);
     if (s == 0) {
       const int g0 = pl.wg_gene[w], g1 = pl.wg_gene[w + 1];
       if (g1 - g0 > gcap || g1 - g0 > pl.gmax) return fail("gene cap", w, g1 - g0);

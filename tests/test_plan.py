@@ -66,10 +66,38 @@ def _links(P, E, seed, R=2, hub=0.0, multi=0.05, both=0.03):
     (300, 5000, (1, 1), -4, 1024, 30.0),       # hub genes
     (1500, 20000, (3840, 3840), -4, 1024, 0.0),  # fold0-like degree, 15 units per CU
     (40, 600, (64, 64), -4, 1024, 0.0),        # few genes: long runs
+    (500, 40000, (1536, 3072), 5, 120, 0.0),   # K=30-like gene cap, long runs (balanced units)
 ])
 def test_plan_invariants(plan_check, P, E, units, gcap, sp_rows, hub):
+    _check(plan_check, P, E, units, gcap, sp_rows, hub)
+
+
+def _check(plan_check, P, E, units, gcap, sp_rows, hub, env=None):
     links = _links(P, E, seed=P + E, hub=hub)
     head = "%d 2 %d %d %d %d %d\n" % (len(links), P, units[0], units[1], gcap, sp_rows)
     body = "\n".join(" ".join(str(v) for v in row) for row in links)
-    res = subprocess.run([plan_check], input=head + body + "\n", capture_output=True, text=True)
+    res = subprocess.run([plan_check], input=head + body + "\n", capture_output=True, text=True,
+                         env=None if env is None else {**os.environ, **env})
     assert res.returncode == 0 and res.stdout.startswith("ok"), res.stdout + res.stderr
+    return res.stdout.split()
+
+
+# large-K plans packed the round-3 way (MMSBM_BALANCE=0: whole runs per unit) keep every invariant
+# but the balance; the balanced plans (default, checked above) split each workgroup evenly
+@pytest.mark.parametrize("P,E,units,gcap,sp_rows,hub", [
+    (40, 600, (1, 1), 33, 16, 0.0),
+    (300, 5000, (1536, 3072), 33, 16, 30.0),
+    (120, 4000, (64, 64), 13, 120, 10.0),
+    (500, 40000, (64, 64), 5, 120, 0.0),       # K=30-like gene cap, long units
+])
+def test_plan_invariants_unbalanced(plan_check, P, E, units, gcap, sp_rows, hub):
+    _check(plan_check, P, E, units, gcap, sp_rows, hub, env={"PLAN_NO_BALANCE": "1"})
+
+
+def test_balanced_plan_fewer_workgroups(plan_check):
+    # K=30-like: 5 genes per workgroup, runs of ~10 chunks, 64-chunk units: the round-3 plan's
+    # units took whole runs up to 64 chunks, so a workgroup's gene cap left most of its 8 units
+    # empty; the balanced plan fills all 8 from fewer workgroups
+    bal = _check(plan_check, 500, 40000, (64, 64), 5, 120, 0.0)
+    old = _check(plan_check, 500, 40000, (64, 64), 5, 120, 0.0, env={"PLAN_NO_BALANCE": "1"})
+    assert int(bal[3]) < int(old[3])

@@ -82,6 +82,26 @@ int fail(int code, const char* fmt, ...) {
 // (GMAX 9 / 4) at 125 us and 1794 us.
 constexpr int lds_target(int K) { return K <= 16 ? 76 * 1024 : 78 * 1024; }
 
+// Pass-A ablations for measurement builds only (results invalid): 1 = no Y stores, 2 = theta
+// gathers from 64 hot rows (L2 hits), 4 = no partial-row stores
+#ifndef MMSBM_ABL
+#define MMSBM_ABL 0
+#endif
+
+// gene_kernel's workgroup kinds interleaved over the grid (1) or in blockIdx order (0, measurement)
+#ifndef MMSBM_GENE_MIX
+#define MMSBM_GENE_MIX 1
+#endif
+
+// Row strides of pass A's V tables and of their genes' theta rows: odd (1) or the round-3 even
+// strides (0, measurement).  The compiler pairs the chunk loop's V reads into ds_read2_b64, whose
+// 16-lane groups bank on (a/4) mod 32: an odd stride puts the 16 rows of a Z read (b = 4 blk + lo)
+// on distinct banks, and the 4 theta rows of a V-prologue read (4 t + lo) likewise; the Z' reads
+// walk one row and stay conflict-free at any stride.
+#ifndef MMSBM_VR_ODD
+#define MMSBM_VR_ODD 1
+#endif
+
 template <int K>
 struct KT {
   static constexpr int NG = (K + 3) / 4;          // 4-wide tiles of one K axis
@@ -89,17 +109,20 @@ struct KT {
   static constexpr int K2 = K * K, K3 = K * K * K;
   static constexpr int NBG = (NG + 3) / 4;        // Z phase: groups of 4 b-tiles (one per block)
   static constexpr int VROWS = 16 * NBG;          // V image rows (b); zero from K on
-  static constexpr int VR = KP + 2;               // row stride: 2 x odd doubles, conflict-free B reads
+  static constexpr int VR = MMSBM_VR_ODD ? KP + 1 : KP + 2;  // V row stride (above)
   static constexpr int VDBL = VROWS * VR;         // one gene's V image
+  static constexpr int TGR = MMSBM_VR_ODD ? KP + 1 : KP;     // theta row stride of the V genes
+  // doubles of g genes' theta rows, even so the wave images after them stay 16-byte aligned
+  static constexpr int tg_dbl(int g) { return (g * TGR + 1) & ~1; }
   static constexpr int TR = KP + 2;               // theta image row stride
   static constexpr int IMG = 8 * TR;              // one chunk: th_u rows of obs 0-3, th_v rows
   static constexpr int SW = (K % 2 == 0) ? 2 : 1;  // staging width: double2 pieces when K is even
   static constexpr int NPC = (8 * KP / SW + 63) / 64;  // staged pieces per lane per chunk
   static constexpr int IMGW = 2 * IMG + 2;        // per wave: double buffer + a dummy piece slot
   static constexpr int IMG_BYTES = NW * IMGW * 8;
-  static constexpr int GMAX_RAW = (lds_target(K) - IMG_BYTES - 64) / ((VDBL + KP) * 8);
+  static constexpr int GMAX_RAW = (lds_target(K) - IMG_BYTES - 64 - 8) / ((VDBL + TGR) * 8);
   static constexpr int GMAX = GMAX_RAW > 64 ? 64 : (GMAX_RAW < 4 ? 4 : GMAX_RAW);
-  static constexpr int LDS_A = GMAX * VDBL * 8 + GMAX * KP * 8 + IMG_BYTES + 64;
+  static constexpr int LDS_A = GMAX * VDBL * 8 + tg_dbl(GMAX) * 8 + IMG_BYTES + 64;
   static constexpr int LDS_B = IMG_BYTES + 64;
   // S partials: (a-tile, group of 4 cell tiles) items over the 8 waves
   static constexpr int NCT = (K2 + 3) / 4;
@@ -303,7 +326,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   // LDS: [gcap V tables][gcap theta rows][per-wave images]; gcap (<= GMAX) = the plan's most
   // genes per workgroup
   double* Tg = smem + gcap * T::VDBL;  // theta rows of the V genes
-  double* img = smem + gcap * (T::VDBL + T::KP) + wv * T::IMGW;
+  double* img = smem + gcap * T::VDBL + T::tg_dbl(gcap) + wv * T::IMGW;
 
   // this wave's unit, and the first records of its pipeline (in flight during the V prologue).
   // Record stream: lane l < 16 holds int l of the chunk's 4 records (i, j, k, w), lane 16 the
@@ -339,7 +362,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     const int ng = wg_gene[w + 1] - wg_gene[w];
     const int* __restrict__ vgw = vgenes + (size_t)w * gcap;
     constexpr bool PV = T::K3 <= NW * T::IMGW;
-    double* Ps = smem + gcap * (T::VDBL + T::KP);
+    double* Ps = smem + gcap * T::VDBL + T::tg_dbl(gcap);
     constexpr int NTG = (T::GMAX * T::KP + NT - 1) / NT, NPV = PV ? (T::K3 + NT - 1) / NT : 1;
     double tg[NTG], pv[NPV];
 #pragma unroll
@@ -359,7 +382,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 #pragma unroll
     for (int i = 0; i < NTG; ++i) {  // theta rows, zero padded
       const int idx = tid + NT * i, gl = idx / T::KP, a = idx % T::KP;
-      if (idx < gcap * T::KP) Tg[idx] = (gl < ng && a < K) ? tg[i] : 0.0;
+      if (idx < gcap * T::KP) Tg[gl * T::TGR + a] = (gl < ng && a < K) ? tg[i] : 0.0;
     }
     if constexpr (PV) {
 #pragma unroll
@@ -405,7 +428,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
         for (int as = 0; as < NG; ++as)
 #pragma unroll
           for (int t = 0; t < GTM; ++t)
-            if (t < GT) acc[t] = mfma4(Tg[(4 * t + lo) * T::KP + 4 * as + hi], bv[u][as], acc[t]);
+            if (t < GT) acc[t] = mfma4(Tg[(4 * t + lo) * T::TGR + 4 * as + hi], bv[u][as], acc[t]);
         const int ct = ctv[u];
 #pragma unroll
         for (int t = 0; t < GTM; ++t) {
@@ -450,7 +473,8 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     for (int t = 0; t < T::NPC; ++t) {
       const int pc = 64 * t + lane;
       const int row8 = pc < 8 * PR ? pc / PR : 0, col = T::SW * (pc % PR);
-      const int g = __shfl(rv, (row8 & 3) * 4 + ((row8 >> 2) ? 2 : 1), 64);
+      int g = __shfl(rv, (row8 & 3) * 4 + ((row8 >> 2) ? 2 : 1), 64);
+      if constexpr (MMSBM_ABL & 2) g &= 63;
       v[t] = *reinterpret_cast<const SV*>(th + (size_t)g * K + (col < K ? col : K - T::SW));
     }
   };
@@ -526,7 +550,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 #pragma unroll
           for (int bg = 0; bg < T::NBG; ++bg) {
             const int bb = 16 * bg + 4 * blk + lo;
-            if (bb < K) yb[(size_t)e1 * K + bb] = c * zb[bg];
+            if (bb < K && !(MMSBM_ABL & 1)) yb[(size_t)e1 * K + bb] = c * zb[bg];
           }
 #pragma unroll
           for (int hg = 0; hg < T::NBG; ++hg) {
@@ -536,7 +560,8 @@ __global__ __launch_bounds__(NT) void pass_kernel(
             for (int bs = 0; bs < NG; ++bs)
               z2 = mfma4(au[bs], V[(4 * bs + hi) * VR + 16 * hg + 4 * blk + lo], z2);
             const int hh = 16 * hg + 4 * blk + lo;
-            if (hh < K) yb[(size_t)e2 * K + hh] = c * z2;
+            if (hh < K && !(MMSBM_ABL & 1)) yb[(size_t)e2 * K + hh] = c * z2;
+            else if (MMSBM_ABL & 1) ll += z2;  // (keep Z' live)
           }
           // ---- M += c th_u (x) th_v over the chunk's 4 observations: one v_mfma_f64_16x16x4 per
           // 16 x 16 tile of M, k = the 4 observations.  Lane l holds A[x = l & 15][o = l >> 4] =
@@ -568,7 +593,8 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                   const int x = 16 * tx + hi + 4 * i, y = 16 * ty + col;
-                  if (x < K && y < K) st_wt(out + x * K + y, m16[tx * NX16 + ty][i]);
+                  if (x < K && y < K && !(MMSBM_ABL & 4)) st_wt(out + x * K + y, m16[tx * NX16 + ty][i]);
+                  else if (MMSBM_ABL & 4) ll += m16[tx * NX16 + ty][i];
                   m16[tx * NX16 + ty][i] = 0.0;
                 }
           }
@@ -580,6 +606,8 @@ __global__ __launch_bounds__(NT) void pass_kernel(
     }
   }
   st_.mark(2);
+  if constexpr (MMSBM_ABL != 0 && EM)  // ablation builds: keep the skipped stores' values live
+    if (ll == -1.2345e300) partL[0] = ll;
   st_.t[5] = (unsigned long long)(c1 - c0);
   st_.t[4] = (unsigned long long)(wg_gene[w + 1] - wg_gene[w]);
   if constexpr (MODE == PASS_LL) {
@@ -687,13 +715,13 @@ template <int K>
 __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const double* __restrict__ prows,
                                          const int* __restrict__ prow_ptr, int P, int R,
                                          long long n_prows, double* __restrict__ x0, double* Ms,
-                                         Stamp& st_) {
+                                         int gw, Stamp& st_) {
   using F = FT<K>;
   constexpr int K2 = F::K2, K3 = K * K * K, NGW = F::NGW, NT = F::NT, KP = F::KP;
   const int tid = threadIdx.x, b = blockIdx.y;
   const int lane = tid & 63, wv = tid >> 6;
   const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
-  const int g0 = blockIdx.x * NGW;
+  const int g0 = gw * NGW;
   const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
   double* Xr = Ms + NGW * F::MSR;  // [KSPLIT][NGW][KP]
   __shared__ int pp[MAX_R][NGW + 1];
@@ -781,7 +809,7 @@ __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const do
     x0[((size_t)b * P + g0 + eg) * K + ex] = X;
   }
   st_.mark(3);
-  st_.flush(2, ((long long)b * gridDim.x + blockIdx.x) * 8 + wv, lane);
+  st_.flush(2, ((long long)b * gridDim.x + gw) * 8 + wv, lane);
 }
 
 // Y part: thread (g, x) = item sums component x of gene g's Y entries [yptr[g], yptr[g + 1]) in
@@ -817,25 +845,41 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
   const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
   Stamp st_{};
   st_.mark(0);
+  // The three workgroup kinds interleaved in proportion over the grid (Bresenham: Y workgroups
+  // among all, then S among the rest), so the HBM-bound Y sums run beside the MFMA-bound gene and
+  // S workgroups instead of after them (dispatch follows blockIdx).  Which kind and index a
+  // workgroup gets never changes what it computes.
+  const long long n_all = (long long)gridDim.x, m = (long long)n_gene_wg + n_sp_wg, n_yw = n_all - m;
+#if MMSBM_GENE_MIX
+  const long long ya = (long long)w * n_yw / n_all;
+  const bool is_y = (long long)(w + 1) * n_yw / n_all > ya;
+  const int j = w - (int)ya;  // index among the gene and S workgroups
+  const int sa = m ? (int)((long long)j * n_sp_wg / m) : 0;
+  const bool is_s = !is_y && m && (long long)(j + 1) * n_sp_wg / m > sa;
+#else  // measurement: gene, S, then Y workgroups in blockIdx order
+  const bool is_y = w >= m, is_s = !is_y && w >= n_gene_wg;
+  const long long ya = w - m;
+  const int j = w, sa = w - n_gene_wg;
+#endif
 #ifdef MMSBM_GENE_ONLY  // measurement builds: run one workgroup kind only (1 gene, 2 S, 4 Y)
   {
-    const int kind = w < n_gene_wg ? 1 : w < n_gene_wg + n_sp_wg ? 2 : 4;
+    const int kind = is_y ? 4 : is_s ? 2 : 1;
     if (!(MMSBM_GENE_ONLY & kind)) return;
   }
 #endif
-  if (w < n_gene_wg) {
-    genes_x0<K>(pr, prows, prow_ptr, P, R, n_prows, x0, Ms, st_);
-  } else if (w < n_gene_wg + n_sp_wg) {
+  if (!is_y && !is_s) {
+    genes_x0<K>(pr, prows, prow_ptr, P, R, n_prows, x0, Ms, j - sa, st_);
+  } else if (is_s) {
     const int lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
-    const int sw = w - n_gene_wg, sp = sw / T::NIG, ig = sw % T::NIG;
+    const int sw = sa, sp = sw / T::NIG, ig = sw % T::NIG;
     const int* d = sp_desc + 3 * sp;
     s_partial<K>(theta + (size_t)b * P * K, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
                  spart + ((size_t)b * n_sp + sp) * T::K3, Ms, ig, tid, wv, hi, blk, lo, st_);
     st_.flush(3, ((long long)b * gridDim.x + w) * NW + wv, lane);
   } else {
-    const long long item = (long long)(w - n_gene_wg - n_sp_wg) * FT<K>::NT + tid;
+    const long long item = ya * FT<K>::NT + tid;
     genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * K, yptr, item, P, ysum + (size_t)b * P * K);
   }
 }
@@ -1245,7 +1289,7 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
     // dynamic LDS for the context's gene cap (<= the compile-time GMAX the opt-in covers)
-    const int lds = c->gcap * (T::VDBL + T::KP) * 8 + T::IMG_BYTES + 64;
+    const int lds = (c->gcap * T::VDBL + T::tg_dbl(c->gcap)) * 8 + T::IMG_BYTES + 64;
     if (mode == PASS_A) {
       if ((rc = lds_opt_in(c, 0, &pass_kernel<K, PASS_A>, T::LDS_A))) return rc;
       pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
@@ -1634,9 +1678,13 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   }
   int rho = 85;  // stream-0 unit length, % of the others' (fused plans; plan.h)
   if (const char* e = getenv("MMSBM_SK_RHO")) rho = std::max(10, std::min(100, atoi(e)));
+  // large-K workgroups: units of even length (plan.h pack_balanced); MMSBM_BALANCE=0 packs whole
+  // runs per unit as in round 3 (measurement)
+  const char* bal = getenv("MMSBM_BALANCE");
+  const bool balance = !(bal && bal[0] == '0');
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
                            c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, 1024, c->sk_fused,
-                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y);
+                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance);
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
   sd.unit_target = c->sk_fused ? units_a : 0;

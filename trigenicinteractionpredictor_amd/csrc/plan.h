@@ -141,6 +141,38 @@ inline void pack_units(const std::vector<int>& run_chunks, int lmax, int gcap, s
   if (cur > 0) ub.push_back(pos);
 }
 
+// Large-K stream-0 packing (the pass kernel's one unit per wave): WORKGROUPS first — whole runs while
+// the workgroup holds at most `gcap` genes (its V tables) and NW * lmax chunks, a run longer than
+// that split into workgroup-sized pieces — then each workgroup's chunks split evenly over its NW
+// units, across gene boundaries (a unit may hold several stretches; a run may span units).  A
+// workgroup lives as long as its longest wave: with one run per unit (pack_units at K = 30 on 10M
+// links: ~5 genes of ~50 chunks per workgroup) 3 of the 8 waves had nothing to do.
+// Returns NW unit boundaries per workgroup (units may be empty when a workgroup has < NW chunks).
+inline void pack_balanced(const std::vector<int>& run_chunks, int lmax, int gcap, std::vector<int>& ub) {
+  ub.assign(1, 0);
+  const int cap = NW * std::max(lmax, 1);
+  int pos = 0, cur = 0, genes = 0, w0 = 0;
+  auto close = [&]() {
+    const long long n = pos - w0;
+    for (int i = 1; i <= NW; ++i) ub.push_back(w0 + (int)(i * n / NW));
+    w0 = pos;
+    cur = 0;
+    genes = 0;
+  };
+  for (int nch : run_chunks) {
+    if (cur > 0 && (genes + 1 > gcap || cur + nch > cap)) close();
+    while (nch > 0) {
+      const int take = std::min(nch, cap - cur);
+      cur += take;
+      pos += take;
+      nch -= take;
+      if (nch > 0) close();  // the run continues in the next workgroup
+    }
+    genes += 1;
+  }
+  if (cur > 0) close();
+}
+
 // Slot layout of a small-K plan (see Plan::sk_*), from the per-unit descriptors and row12.
 inline void make_slots(Plan& pl) {
   const int R = pl.R;
@@ -227,7 +259,7 @@ inline void make_slots(Plan& pl) {
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
                   int wg_target = 1024, bool fill = false, int gu = GU, int rho_pct = 85,
-                  bool yent = false) {
+                  bool yent = false, bool balance = true) {
   Plan pl;
   pl.gu = std::max(1, std::min(gu, GU));
   pl.R = R;
@@ -331,8 +363,12 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       }
       // units
       std::vector<int> ub;
-      pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? pl.gu : s == 0 ? gcap : (1 << 30), ub,
-                 small && fill);
+      const bool bal = balance && !small && s == 0;  // units NW per workgroup, even lengths
+      if (bal)
+        pack_balanced(run_chunks, lmax_a, gcap, ub);
+      else
+        pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? pl.gu : s == 0 ? gcap : (1 << 30), ub,
+                   small && fill);
       const int nunits = (int)ub.size() - 1;
       // chunk -> gene
       const int nch = ub.empty() ? 0 : ub.back();
@@ -376,7 +412,9 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       } else {
         // workgroups: NW consecutive units; stream 0 also caps the distinct genes (V table)
         std::vector<int> wstart;  // unit index where each workgroup starts
-        {
+        if (bal) {
+          for (int u = 0; u < nunits; u += NW) wstart.push_back(u);
+        } else {
           int u = 0;
           while (u < nunits) {
             wstart.push_back(u);
