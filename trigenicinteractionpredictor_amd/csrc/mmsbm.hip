@@ -88,9 +88,30 @@ constexpr int lds_target(int K) { return K <= 16 ? 76 * 1024 : 78 * 1024; }
 #define MMSBM_ABL 0
 #endif
 
-// gene_kernel's workgroup kinds interleaved over the grid (1) or in blockIdx order (0, measurement)
+// Large-K Y entries: row stride K rounded up to MMSBM_YALIGN doubles (4 = one 32-B sector), so no
+// entry starts inside a sector another entry also writes (the pad words hold zeros or never-read
+// values).  K=30 on 10M links: pass A 3,695 us at stride 30, 3,402 at 32; K=20 x 8 (already
+// sector-aligned at 20): 139.8 us at 20, 152.5 at 24 and 197.0 at 32, the pad being pure extra
+// bytes there (profiles/r04p_large_ab.txt).
+#ifndef MMSBM_YALIGN
+#define MMSBM_YALIGN 4
+#endif
+constexpr int y_stride(int K) { return (K + MMSBM_YALIGN - 1) / MMSBM_YALIGN * MMSBM_YALIGN; }
+
+// Pass-kernel occupancy hint: 1 leaves the compiler free (K = 25-32 take 132-134 VGPRs, so one
+// 8-wave workgroup per CU although the LDS would fit two); 4 caps it at 128 VGPRs (4 waves per
+// SIMD) at the price of 3-21 spilled VGPRs: K=30 pass A 3,402 us capped vs 3,306 free
+// (profiles/r04p_large_ab.txt), so the default stays free.
+#ifndef MMSBM_PASS_WPE
+#define MMSBM_PASS_WPE 1
+#endif
+constexpr int PASS_WPE = MMSBM_PASS_WPE;
+
+// gene_kernel's workgroup kinds in blockIdx order: gene, S, then Y workgroups (0), or interleaved
+// in proportion over the grid (1, measurement: K=20 x 8 gene kernel 120 vs 74 us, K=30 1,938 vs
+// 1,348 us, profiles/r04n_ablations.txt — the Y workgroups then hold CUs the MFMA-bound kinds need)
 #ifndef MMSBM_GENE_MIX
-#define MMSBM_GENE_MIX 1
+#define MMSBM_GENE_MIX 0
 #endif
 
 // Row strides of pass A's V tables and of their genes' theta rows: odd (1) or the round-3 even
@@ -145,12 +166,15 @@ __device__ __forceinline__ d4v mfma16(double a, double b, d4v c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Stores of the per-iteration intermediates (c, partial rows, S partials, the p snapshot) write
-// through the XCD L2 (agent-scope relaxed atomic store = global_store sc1): their bytes leave L2
-// while the kernel runs instead of being written back at the kernel boundary.  -DMMSBM_WT=0
-// builds plain stores (measurement).
+// Stores of the large-K intermediates (partial rows, S partials): plain (0), or written through
+// the XCD L2 (1: agent-scope relaxed atomic store = global_store sc1, so their bytes leave L2
+// while the kernel runs instead of at the kernel boundary).  Write-through won 2-3 % at fold0 in
+// round 2, when the large-K kernels ran the headline with c and the S partials among these
+// stores; since round 4 (stream 0 + Y entries) it costs: pass A 3,402 -> 2,776 us at K=30 on 10M
+// links and 152.5 -> 128.3 us at K=20 x 8 with plain stores (profiles/r04p_large_ab.txt), a
+// partial row's K x K words being written as scattered 4 x 16-word pieces.
 #ifndef MMSBM_WT
-#define MMSBM_WT 1
+#define MMSBM_WT 0
 #endif
 __device__ __forceinline__ void st_wt(double* p, double v) {
   if constexpr (MMSBM_WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -300,7 +324,7 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
 // and per gene stretch the M^0 partial row (K^2) for X^0 and S (gene_kernel).
 // ------------------------------------------------------------------------------------------
 template <int K, int MODE>
-__global__ __launch_bounds__(NT) void pass_kernel(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) void pass_kernel(
     const int4* __restrict__ rows, const int* __restrict__ chunk_prow,
     const int* __restrict__ chunk_vslot, const int* __restrict__ row_y, const int* __restrict__ wg_units,
     const int* __restrict__ wg_code, const int* __restrict__ wg_gene, const int* __restrict__ vgenes,
@@ -452,7 +476,9 @@ __global__ __launch_bounds__(NT) void pass_kernel(
   st_.mark(1);
 
   double* __restrict__ pb = prows + (size_t)b * n_prows * T::K2;
-  double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * K;
+  constexpr int YS = y_stride(K);
+  static_assert(YS <= 16 * T::NBG, "Y stride within the Z / Z' lanes");
+  double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * YS;
   // staged pieces of one chunk: piece pc = 64 t + lane is SW doubles of row8 = pc / (KP / SW)
   // (rows 0-3: th_u = th_j of obs 0-3, rows 4-7: th_v = th_k), columns SW (pc % (KP / SW)) ..
   typedef double d2v __attribute__((ext_vector_type(2)));  // a native vector: SROA-friendly
@@ -550,17 +576,18 @@ __global__ __launch_bounds__(NT) void pass_kernel(
 #pragma unroll
           for (int bg = 0; bg < T::NBG; ++bg) {
             const int bb = 16 * bg + 4 * blk + lo;
-            if (bb < K && !(MMSBM_ABL & 1)) yb[(size_t)e1 * K + bb] = c * zb[bg];
+            if (bb < YS && !(MMSBM_ABL & 1)) yb[(size_t)e1 * YS + bb] = c * zb[bg];
           }
 #pragma unroll
           for (int hg = 0; hg < T::NBG; ++hg) {
             double z2 = 0.0;
-            // (columns h >= K of V are zero, past KP the next row's words: finite, never stored)
+            // (columns h in [K, KP) of V are zero; the pad column and the next row's words past
+            // KP reach only Y pad words, which nothing reads)
 #pragma unroll
             for (int bs = 0; bs < NG; ++bs)
               z2 = mfma4(au[bs], V[(4 * bs + hi) * VR + 16 * hg + 4 * blk + lo], z2);
             const int hh = 16 * hg + 4 * blk + lo;
-            if (hh < K && !(MMSBM_ABL & 1)) yb[(size_t)e2 * K + hh] = c * z2;
+            if (hh < YS && !(MMSBM_ABL & 1)) yb[(size_t)e2 * YS + hh] = c * z2;
             else if (MMSBM_ABL & 1) ll += z2;  // (keep Z' live)
           }
           // ---- M += c th_u (x) th_v over the chunk's 4 observations: one v_mfma_f64_16x16x4 per
@@ -825,7 +852,7 @@ __device__ __forceinline__ void genes_ysum(const double* __restrict__ yb, const 
   for (int e = e0; e < e1; e += YU) {
     double v[YU];
 #pragma unroll
-    for (int u = 0; u < YU; ++u) v[u] = yb[(size_t)(e + u < e1 ? e + u : e) * K + x];
+    for (int u = 0; u < YU; ++u) v[u] = yb[(size_t)(e + u < e1 ? e + u : e) * y_stride(K) + x];
 #pragma unroll
     for (int u = 0; u < YU; ++u)
       if (e + u < e1) S += v[u];
@@ -845,10 +872,9 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
   const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
   Stamp st_{};
   st_.mark(0);
-  // The three workgroup kinds interleaved in proportion over the grid (Bresenham: Y workgroups
-  // among all, then S among the rest), so the HBM-bound Y sums run beside the MFMA-bound gene and
-  // S workgroups instead of after them (dispatch follows blockIdx).  Which kind and index a
-  // workgroup gets never changes what it computes.
+  // Workgroup kind and index from blockIdx (MMSBM_GENE_MIX above; the interleaved form is
+  // Bresenham: Y workgroups among all, then S among the rest).  Which kind and index a workgroup
+  // gets never changes what it computes.
   const long long n_all = (long long)gridDim.x, m = (long long)n_gene_wg + n_sp_wg, n_yw = n_all - m;
 #if MMSBM_GENE_MIX
   const long long ya = (long long)w * n_yw / n_all;
@@ -859,7 +885,7 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
 #else  // measurement: gene, S, then Y workgroups in blockIdx order
   const bool is_y = w >= m, is_s = !is_y && w >= n_gene_wg;
   const long long ya = w - m;
-  const int j = w, sa = w - n_gene_wg;
+  const int j = w, sa = is_s ? w - n_gene_wg : 0;  // (j - sa: the gene workgroup index)
 #endif
 #ifdef MMSBM_GENE_ONLY  // measurement builds: run one workgroup kind only (1 gene, 2 S, 4 Y)
   {
@@ -880,7 +906,7 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
     st_.flush(3, ((long long)b * gridDim.x + w) * NW + wv, lane);
   } else {
     const long long item = ya * FT<K>::NT + tid;
-    genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * K, yptr, item, P, ysum + (size_t)b * P * K);
+    genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
   }
 }
 
@@ -1228,7 +1254,7 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   // large-K: Y entries (+ the dummy entry of padding rows), M^0 partial rows, S partials, x0 and
   // ysum, likelihood partials, fin's sums-out scratch
   L.cbuf = off;
-  off += align_up(B * (tr.n_y + 1) * c->K * 8);
+  off += align_up(B * (tr.n_y + 1) * y_stride(c->K) * 8);
   L.prows = off;
   off += align_up(B * std::max<long long>(tr.n_prows, 1) * K2 * 8);
   L.spart = off;

@@ -41,6 +41,9 @@ enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
 #ifndef MMSBM_SK_MRED
 #define MMSBM_SK_MRED 0  // 1: d's sum over b on MFMA, four chunks at a time (measured slower than the DPP row sum)
 #endif
+#ifndef MMSBM_SK_PVS
+#define MMSBM_SK_PVS 1  // P^s rows at an odd stride (0: K^2, round 3), see SKT::PVS
+#endif
 #ifndef MMSBM_SK_GHOIST
 #define MMSBM_SK_GHOIST 0  // 1: the first block's theta gathers before the V tables (after the barrier)
 #endif
@@ -56,10 +59,14 @@ struct SKT {
   static constexpr int NCT = (K2 + 3) / 4;        // 4-cell tiles of a dense K x K row
   static constexpr int NCG = (NCT + 3) / 4;       // groups of 4 cell tiles (one MFMA, 4 blocks)
   static constexpr int SLOT = 4 * NCT;            // doubles per stretch slot (V table, then M row)
-  // P^s_r staged per workgroup, plain [z][cell] order, zero past K^3 up to the last word the
-  // unguarded V-operand reads touch (rows a >= K of the 4-wide a tiles, cells up to 16 NCG)
-  static constexpr int PVR = (K - 1) * K2 + 16 * NCG;  // (V-operand rows a >= K read row K - 1)
-  static constexpr int PSD = ((PVR > K3 ? PVR : K3) + 1) & ~1;
+  // P^s_r staged per workgroup, [z][cell] rows of PVS words (zero past K^2 and past the last row,
+  // up to the last word the unguarded V-operand reads touch: rows a >= K of the 4-wide a tiles,
+  // cells up to 16 NCG).  The X contraction's B reads take 16 rows z at once, paired into
+  // ds_read2_b64 (16-lane groups, bank (a/4) mod 32): at the K^2 stride (100 at K = 10) rows
+  // z, z + 4, z + 8 shared banks, an odd stride puts the 16 rows on distinct banks.
+  static constexpr int PVS = MMSBM_SK_PVS ? (K2 | 1) : K2;
+  static constexpr int PVR = (K - 1) * PVS + 16 * NCG;  // (V-operand rows a >= K read row K - 1)
+  static constexpr int PSD = ((PVR > K * PVS ? PVR : K * PVS) + 1) & ~1;
   static constexpr int GUK = mmsbm_plan::sk_gu(K);  // stretches per unit (slots per wave): 8 or 4
   static constexpr int NT2 = GUK / 4;                // 4-row MFMA tiles of the unit's stretches
   static constexpr int THL = GUK * 4 * NG;          // the unit's pivot-gene theta rows (S operand)
@@ -140,7 +147,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
   const int s = __builtin_amdgcn_readfirstlane(sr / R), r = __builtin_amdgcn_readfirstlane(sr % R);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-  double* PV = smem;  // P^s_r[z][cell] (cell = x K + y over the u, v slots), zero past K^3
+  double* PV = smem;  // P^s_r[z][cell] (cell = x K + y over the u, v slots), rows of SKT::PVS words
   double* wl = smem + T::PSD + wv * (MODE == SK_B ? T::WAVE_B : MODE == SK_U ? T::WAVE_U : T::WAVE);
   constexpr int GUK = T::GUK, NT2 = T::NT2;
   double* MSl = wl;                                                 // GUK slots: V, then M
@@ -162,9 +169,9 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
   double pvv[T::NPV];
 #pragma unroll
   for (int i = 0; i < T::NPV; ++i) {
-    const int e = tid + NT * i;
-    const bool ok = e < K3;
-    const int z = ok ? e / K2 : 0, x = ok ? (e % K2) / K : 0, y = ok ? e % K : 0;
+    const int e = tid + NT * i, z = e / T::PVS, cell = e % T::PVS;
+    const bool ok = z < K && cell < K2;
+    const int x = ok ? cell / K : 0, y = ok ? cell % K : 0;
     const double v = p[ok ? sk_pidx<K>(s, z, x, y) : 0];
     pvv[i] = ok ? v : 0.0;
   }
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
           if (live) {
 #pragma unroll
             for (int as = 0; as < NG; ++as)  // (rows a >= K: zero theta times row K - 1)
-              v = mfma4(tv[tt][as], PV[(4 * as + hi < K ? 4 * as + hi : K - 1) * K2 + cell], v);
+              v = mfma4(tv[tt][as], PV[(4 * as + hi < K ? 4 * as + hi : K - 1) * T::PVS + cell], v);
           }
           if (cell < SLOT) MSl[(4 * tt + hi) * SLOT + cell] = cell < K2 ? v : 0.0;
         }
@@ -464,7 +471,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
       // block's z tile, k = 4 cells per step)
       // (four independent accumulator chains over the cell steps, added in a fixed order)
       const int z = 4 * blk + lo;
-      const double* __restrict__ pz = PV + (z < K ? z : K - 1) * K2 + hi;  // B: P^s[z][4 ks + hi]
+      const double* __restrict__ pz = PV + (z < K ? z : K - 1) * T::PVS + hi;  // B: P^s[z][4 ks + hi]
 #pragma unroll
       for (int tt = 0; tt < NT2; ++tt) {
         if (tt == 0 || nst > 4 * tt) {  // (uniform)
@@ -649,7 +656,7 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
   const int r = __builtin_amdgcn_readfirstlane(sr);
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-  double* PV = smem;  // P^0_r[z][cell] (cell = x K + y), zero past K^3
+  double* PV = smem;  // P^0_r[z][cell] (cell = x K + y), rows of SKT::PVS words
   double* wl = smem + T::PSD + wv * Y::WAVE;
   double* MSl = wl;                                        // GUK slots: V, then M
   int2* REC = reinterpret_cast<int2*>(wl + GUK * SLOT);    // the block's (u, v) genes
@@ -666,9 +673,10 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
   double pvv[T::NPV];
 #pragma unroll
   for (int i = 0; i < T::NPV; ++i) {
-    const int e = tid + NT * i;
-    const double v = p[e < K3 ? e : 0];
-    pvv[i] = e < K3 ? v : 0.0;
+    const int e = tid + NT * i, z = e / T::PVS, cell = e % T::PVS;
+    const bool ok = z < K && cell < K2;
+    const double v = p[ok ? z * K2 + cell : 0];
+    pvv[i] = ok ? v : 0.0;
   }
 
   const long long slot = (long long)w * NW + wv;
@@ -771,7 +779,7 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
         if (live) {
 #pragma unroll
           for (int as = 0; as < NG; ++as)
-            v = mfma4(tv[tt][as], PV[(4 * as + hi < K ? 4 * as + hi : K - 1) * K2 + cell], v);
+            v = mfma4(tv[tt][as], PV[(4 * as + hi < K ? 4 * as + hi : K - 1) * T::PVS + cell], v);
         }
         if (cell < SLOT) MSl[(4 * tt + hi) * SLOT + cell] = cell < K2 ? v : 0.0;
       }
@@ -867,7 +875,7 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
     st_.mark(2);
     // ---- X_q[z] = sum_cell P^0[z][cell] M_q[cell] for the unit's rows q
     const int z = 4 * blk + lo;
-    const double* __restrict__ pz = PV + (z < K ? z : K - 1) * K2 + hi;
+    const double* __restrict__ pz = PV + (z < K ? z : K - 1) * T::PVS + hi;
 #pragma unroll
     for (int tt = 0; tt < NT2; ++tt) {
       if (tt == 0 || nst > 4 * tt) {
