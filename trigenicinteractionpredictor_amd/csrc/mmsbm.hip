@@ -80,7 +80,12 @@ int fail(int code, const char* fmt, ...) {
 // Measured (tools/gpu_r02c_gcap.sh): a 150 KB budget (one workgroup per CU, GMAX 22 at K = 20,
 // 13 at K = 30) ran pass A at 156 us (K = 20 x 8) and 2088 us (K = 30, 10M links); 78 KB
 // (GMAX 9 / 4) at 125 us and 1794 us.
-constexpr int lds_target(int K) { return K <= 16 ? 76 * 1024 : 78 * 1024; }
+// -DMMSBM_LDS_BIG=k: a one-workgroup-per-CU budget (150 KB) from K = k up (measurement: at K >= 25
+// the pass kernel takes more than 128 VGPRs and runs one workgroup per CU anyway)
+#ifndef MMSBM_LDS_BIG
+#define MMSBM_LDS_BIG 99
+#endif
+constexpr int lds_target(int K) { return K >= MMSBM_LDS_BIG ? 150 * 1024 : K <= 16 ? 76 * 1024 : 78 * 1024; }
 
 // Pass-A ablations for measurement builds only (results invalid): 1 = no Y stores, 2 = theta
 // gathers from 64 hot rows (L2 hits), 4 = no partial-row stores
@@ -860,6 +865,17 @@ __device__ __forceinline__ void genes_ysum(const double* __restrict__ yb, const 
   ysum_b[item] = S;
 }
 
+// The Y sums as a launch of their own (no LDS), on a second stream beside gene_kernel
+// (MMSBM_YSPLIT=1, measurement): HBM-bound Y sums beside the MFMA / L2-bound gene and S
+// workgroups.  Measured no faster (mmsbm_ctx::ysplit).
+template <int K>
+__global__ __launch_bounds__(256) void ysum_kernel(const double* __restrict__ ybuf, const int* __restrict__ yptr,
+                                                   double* __restrict__ ysum, int P, long long n_y) {
+  const int b = blockIdx.y;
+  const long long item = (long long)blockIdx.x * 256 + threadIdx.x;
+  genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
+}
+
 template <int K>
 __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>::WPE))) void gene_kernel(
     const double* __restrict__ theta, const double* __restrict__ pr, const double* __restrict__ prows,
@@ -1213,6 +1229,13 @@ struct mmsbm_ctx {
   bool warm = false;                 // a direct iteration ran (LDS opt-ins done before capture)
   hipStream_t cap = nullptr;         // capture stream (torch's default stream cannot be captured)
   hipGraphExec_t gexec = nullptr;
+  // large-K Y sums inside gene_kernel, or (MMSBM_YSPLIT=1, measurement) as ysum_kernel on a second
+  // stream forked from the caller's after pass A and joined before the update: no overlap gained
+  // (K=30 gene 1,930 vs 1,928 us; K=20 x 8 128 vs 113 us, profiles/r04r_ysplit_ab.txt) — the gene
+  // kernel's waves leave a CU no VGPRs for the Y waves
+  bool ysplit = false;
+  hipStream_t ys = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   const double *g_theta = nullptr, *g_pr = nullptr;
   unsigned long long g_gen = 0;
   int g_iters = 0;
@@ -1306,12 +1329,29 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
   if (mode == PASS_B) {  // launch 2: the gene kernel (x0, S partials, Y sums) of the train plan
     const int ngw = (c->P + F::NGW - 1) / F::NGW;
     const int nspw = std::max(h.n_sp, 1) * T::NIG;
-    const int nyw = (int)(((long long)c->P * K + F::NT - 1) / F::NT);
+    const int nyw = c->ysplit ? 0 : (int)(((long long)c->P * K + F::NT - 1) / F::NT);
     if ((rc = lds_opt_in(c, 8, &gene_kernel<K>, F::LDS))) return rc;
     const size_t pk = (size_t)c->B * c->P * K;
+    if (c->ysplit) {  // the Y sums on the second stream, from the same point of the caller's stream
+      if (!c->ys) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->ys, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+      }
+      HIP_TRY(hipEventRecord(c->ev_fork, s));
+      HIP_TRY(hipStreamWaitEvent(c->ys, c->ev_fork, 0));
+      const long long nyb = ((long long)c->P * K + 255) / 256;
+      ysum_kernel<K><<<dim3((unsigned)nyb, c->B), 256, 0, c->ys>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
+      HIP_TRY(hipGetLastError());
+    }
     gene_kernel<K><<<dim3(ngw + nspw + nyw, c->B), F::NT, F::LDS, s>>>(
         theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
         c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, nspw);
+    if (c->ysplit) {
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(c->ev_join, c->ys));
+      HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    }
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
     // dynamic LDS for the context's gene cap (<= the compile-time GMAX the opt-in covers)
@@ -1562,6 +1602,7 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   auto* c = new mmsbm_ctx();
   c->device = device;
   if (const char* gi = getenv("MMSBM_GRAPH")) c->graph_iters = std::max(0, atoi(gi));
+  if (const char* ysp = getenv("MMSBM_YSPLIT")) c->ysplit = ysp[0] != '0';
   if (MMSBM_STAMP && getenv("MMSBM_STAMP")) {
     DeviceGuard g(device);
     const size_t bytes = sizeof(unsigned long long) * 5 * STAMP_WAVES * STAMP_SLOTS;
@@ -1581,6 +1622,9 @@ int mmsbm_destroy(mmsbm_ctx* c) {
   if (c->stamp) (void)hipFree(c->stamp);
   if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
   if (c->cap) (void)hipStreamDestroy(c->cap);
+  if (c->ys) (void)hipStreamDestroy(c->ys);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (auto& v : c->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   delete c;
