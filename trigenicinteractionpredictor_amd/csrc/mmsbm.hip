@@ -80,10 +80,11 @@ int fail(int code, const char* fmt, ...) {
 // Measured (tools/gpu_r02c_gcap.sh): a 150 KB budget (one workgroup per CU, GMAX 22 at K = 20,
 // 13 at K = 30) ran pass A at 156 us (K = 20 x 8) and 2088 us (K = 30, 10M links); 78 KB
 // (GMAX 9 / 4) at 125 us and 1794 us.
-// -DMMSBM_LDS_BIG=k: a one-workgroup-per-CU budget (150 KB) from K = k up (measurement: at K >= 25
-// the pass kernel takes more than 128 VGPRs and runs one workgroup per CU anyway)
+// From K = MMSBM_LDS_BIG up the pass kernel takes more than 128 VGPRs (130-140 at K = 25-32), so it
+// runs one workgroup per CU whatever its LDS: there the budget is 150 KB (GMAX 13 at K = 30 instead
+// of 5; pass A 2,761 -> 2,531 us at K=30 on 10M links, profiles/r04s_large_ab.txt)
 #ifndef MMSBM_LDS_BIG
-#define MMSBM_LDS_BIG 99
+#define MMSBM_LDS_BIG 25
 #endif
 constexpr int lds_target(int K) { return K >= MMSBM_LDS_BIG ? 150 * 1024 : K <= 16 ? 76 * 1024 : 78 * 1024; }
 
@@ -111,6 +112,11 @@ constexpr int y_stride(int K) { return (K + MMSBM_YALIGN - 1) / MMSBM_YALIGN * M
 #define MMSBM_PASS_WPE 1
 #endif
 constexpr int PASS_WPE = MMSBM_PASS_WPE;
+
+// gene_kernel fill rounds: partial rows per entry loaded together (0 = FT's choice; measurement)
+#ifndef MMSBM_GENE_RW
+#define MMSBM_GENE_RW 0
+#endif
 
 // gene_kernel's workgroup kinds in blockIdx order: gene, S, then Y workgroups (0), or interleaved
 // in proportion over the grid (1, measurement: K=20 x 8 gene kernel 120 vs 74 us, K=30 1,938 vs
@@ -288,15 +294,17 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
       if (tid + NT * i < QB * T::KP) Tq[tid + NT * i] = x[i];
     __syncthreads();
     st_.mark(1);
-    for (int qq = 0; qq < nq; qq += 4 * RS) {  // RS steps of 4 rows per round, loads together
-      double m[RS];
+    // RS steps of 4 rows per round, double-buffered: the next round's partial-row loads are in
+    // flight during this round's MFMAs.  Rows past nq load row 0 of the block (finite) against
+    // zero theta rows; an invalid cell loads cell 0 and is never stored.
+    auto ldm = [&](int qq, double (&m)[RS]) {
 #pragma unroll
       for (int u = 0; u < RS; ++u) {
         const int row = qq + 4 * u + hi;
-        const bool vq = row < nq;
-        const double v = prows_b[(size_t)(qb + (vq ? row : 0)) * T::K2 + cellc];
-        m[u] = (vq && cv) ? v : 0.0;
+        m[u] = prows_b[(size_t)(qb + (row < nq ? row : 0)) * T::K2 + cellc];
       }
+    };
+    auto mma = [&](int qq, const double (&m)[RS]) {
 #pragma unroll
       for (int u = 0; u < RS; ++u) {
         const int row = qq + 4 * u + hi;  // Tq rows past nq (and past QB) read as zero
@@ -304,6 +312,14 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
 #pragma unroll
         for (int t = 0; t < NG; ++t) acc[t] = mfma4(row < QB ? tq[4 * t + lo] : 0.0, m[u], acc[t]);
       }
+    };
+    double mA[RS], mB[RS];
+    ldm(0, mA);
+    for (int qq = 0; qq < nq; qq += 8 * RS) {
+      ldm(qq + 4 * RS, mB);
+      mma(qq, mA);
+      ldm(qq + 8 * RS, mA);
+      if (qq + 4 * RS < nq) mma(qq + 4 * RS, mB);
     }
   }
   if (cgv) {
@@ -702,6 +718,9 @@ struct FT {
   static constexpr int RE_CAP = TWO ? 6 : 12;
   static constexpr int WPE = TWO ? 4 : 1;
   static constexpr int YU = 8;                  // Y entries in flight per thread
+  // partial rows of one (gene, cell) entry loaded together per fill round (balanced plans give a
+  // gene about 2.4 rows per rating at K = 30; rows past these are summed one dependent load at a time)
+  static constexpr int RW = MMSBM_GENE_RW ? MMSBM_GENE_RW : TWO ? 2 : 4;
   static_assert(NXG * KSPLIT == 8, "gene part: one (a group, k part) per wave");
   static_assert(NGW * K <= NT, "gene part epilogue: one (gene, a) per thread");
   static_assert(LDS <= 160 * 1024, "gene kernel LDS over budget");
@@ -717,26 +736,37 @@ __device__ __forceinline__ void x0_tiles(const double* __restrict__ Mg, const do
   using F = FT<K>;
   constexpr int K2 = K * K, UB = 8, GT = F::GT;
   const int ac = a < K ? a : K - 1;
-#pragma unroll 1
-  for (int ks0 = kb; ks0 < ke; ks0 += UB) {
-    double bv[UB];
-    int kk[UB];
+  // batches of UB k-steps, double-buffered: the next batch's p loads (L2) are in flight during
+  // this batch's MFMAs (a batch past ke loads clamped addresses and is not used)
+  auto ld = [&](int ks0, double (&bv)[UB]) {
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int ks = ks0 + u < ke ? ks0 + u : ke - 1;
       const int k = 4 * ks + hi, kc = k < K2 ? k : K2 - 1;
       bv[u] = p[ac * K2 + kc];
-      kk[u] = k;
     }
+  };
+  auto mm = [&](int ks0, const double (&bv)[UB]) {
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const bool ok = ks0 + u < ke;
+      const int k = 4 * (ok ? ks0 + u : kb) + hi;
 #pragma unroll
       for (int t = 0; t < GT; ++t) {
-        const double m = Mg[t * 4 * F::MSR + kk[u]];
+        const double m = Mg[t * 4 * F::MSR + k];
         acc[t] = mfma4(ok ? m : 0.0, bv[u], acc[t]);
       }
     }
+  };
+  if (kb >= ke) return;
+  double bA[UB], bB[UB];
+  ld(kb, bA);
+#pragma unroll 1
+  for (int ks0 = kb; ks0 < ke; ks0 += 2 * UB) {
+    ld(ks0 + UB, bB);
+    mm(ks0, bA);
+    ld(ks0 + 2 * UB, bA);
+    if (ks0 + UB < ke) mm(ks0 + UB, bB);
   }
 }
 
@@ -774,7 +804,8 @@ __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const do
   // round in flight (addresses clamped, loads unconditional); the first round of the next rating
   // is loaded before this rating's contraction, so its latency hides under the MFMAs.  Only the
   // loaded values stay live; ranges are re-read from LDS when the round is stored.
-  double v1[RE], v2[RE];
+  constexpr int RW = F::RW;
+  double vr[RW][RE];
   auto entry = [&](int r, int idx, int& qa, int& qb, int& kk) {
     const int gl = idx / F::K2P, k = idx % F::K2P;
     const bool ok = idx < NE && k < K2;
@@ -787,8 +818,8 @@ __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const do
     for (int u = 0; u < RE; ++u) {
       int qa, qb, kk;
       entry(r, i0 + u * NT, qa, qb, kk);
-      v1[u] = pb[(size_t)(qa < qb ? qa : 0) * K2 + kk];
-      v2[u] = pb[(size_t)(qa + 1 < qb ? qa + 1 : 0) * K2 + kk];
+#pragma unroll
+      for (int j = 0; j < RW; ++j) vr[j][u] = pb[(size_t)(qa + j < qb ? qa + j : 0) * K2 + kk];
     }
   };
   auto store_round = [&](int r, int i0) {
@@ -797,9 +828,11 @@ __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const do
       const int idx = i0 + u * NT;
       int qa, qb, kk;
       entry(r, idx, qa, qb, kk);
-      double m = qa < qb ? v1[u] : 0.0;
-      if (qa + 1 < qb) m += v2[u];
-      for (int q = qa + 2; q < qb; ++q) m += pb[(size_t)q * K2 + kk];
+      double m = qa < qb ? vr[0][u] : 0.0;  // rows in order
+#pragma unroll
+      for (int j = 1; j < RW; ++j)
+        if (qa + j < qb) m += vr[j][u];
+      for (int q = qa + RW; q < qb; ++q) m += pb[(size_t)q * K2 + kk];
       if (idx < NE) Ms[(idx / F::K2P) * F::MSR + idx % F::K2P] = m;
     }
   };
@@ -1752,8 +1785,12 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   // runs per unit as in round 3 (measurement)
   const char* bal = getenv("MMSBM_BALANCE");
   const bool balance = !(bal && bal[0] == '0');
+  // stream-0 partial rows per S partial at large K (each S partial is K^3 words the update sums);
+  // MMSBM_SP_ROWS=n overrides it (measurement)
+  int sp_rows = c->K <= 12 ? 16 : 4 * c->K;
+  if (const char* e = getenv("MMSBM_SP_ROWS")) sp_rows = std::max(4, atoi(e));
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
-                           c->gcap, c->K <= 12 ? 16 : 4 * c->K, c->sk, 1024, c->sk_fused,
+                           c->gcap, sp_rows, c->sk, 1024, c->sk_fused,
                            mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance);
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
