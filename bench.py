@@ -117,7 +117,7 @@ def spawn_ranks(n):
 
 KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, Z', d, c, the j / k Y entries, M0 "
                           "partial rows; FP64 MFMA)",
-                "gene": "gene_kernel<%d> (X0 contractions on FP64 MFMA, S partials) + ysum_kernel (Y entry sums, second stream)",
+                "gene": "gene_kernel<%d> (X0 contractions on FP64 MFMA) + gene_sy_kernel (S partials, Y entry sums)",
                 "fused": "fused E-step: sky_pass_kernel<%d> (SK_Y, stream 0: V, Z, Z', d, c, Y entries, "
                          "M, X, S partials) / sk_pass_kernel<K, SK_U> (3 streams); FP64 MFMA",
                 "pass_b": "sk_pass_kernel<%d, SK_B> (streams 1/2: M1, M2, X)",

@@ -13,6 +13,7 @@ import sys
 
 NAMES = {"pass_kernel<%d, 0>": "pass_a", "gene_kernel<%d>": "gene", "upd_kernel<%d, false>": "fin",
          "ysum_kernel<%d>": "ysum",  # (large-K Y sums, on a second stream beside gene_kernel)
+         "gene_sy_kernel<%d>": "gene_sy",  # (large-K S + Y workgroups, the gene label's second launch)
          # small-K kernels (csrc/sk.h), labelled as EMEngine.LABELS names them
          "sky_pass_kernel<%d>": "fused", "sk_pass_kernel<%d, 3>": "fused", "sk_pass_kernel<%d, 0>": "pass_a",
          "sk_pass_kernel<%d, 2>": "pass_b", "sk_fin_kernel<%d, false>": "fin"}
@@ -42,9 +43,11 @@ def main(root, K, E_obs, B, out):
         if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
             rec["hbm_bytes_per_launch"][key] = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
     hb = rec["hbm_bytes_per_launch"]
-    if "ysum" in hb and "gene" in hb:  # the gene label's launch = gene_kernel + ysum_kernel
+    # the gene label = gene_kernel + the S / Y launches beside or after it
+    extra = [k for k in ("ysum", "gene_sy") if k in hb]
+    if extra and "gene" in hb:
         hb["gene_kernel_only"] = hb["gene"]
-        hb["gene"] += hb["ysum"]
+        hb["gene"] += sum(hb[k] for k in extra)
     with open(out, "w") as f:
         json.dump(rec, f, indent=1, sort_keys=True)
     print(json.dumps(rec["hbm_bytes_per_launch"], indent=1))

@@ -260,7 +260,7 @@ enum { PASS_A = 0, PASS_LL = 1, PASS_B = 2 };  // (PASS_B: the small-K family's 
 // blocks = four cell tiles; wave wv of item group ig owns cell group cg = ig NW + wv (16 cells)
 // for every a tile, so each partial-row value is loaded once and feeds NG MFMAs.
 // ------------------------------------------------------------------------------------------
-template <int K>
+template <int K, int RS>
 __device__ __forceinline__ void s_partial(const double* __restrict__ th, const double* __restrict__ prows_b,
                                           const int* __restrict__ prow_gene, int q0, int q1,
                                           double* __restrict__ out, double* __restrict__ Tq, int ig,
@@ -269,7 +269,7 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
   constexpr int NG = T::NG;
   // blocks of QB partial rows: their genes' theta rows staged in LDS (zero padded), so the loop
   // over the block only streams the partial rows themselves
-  constexpr int QB = 64, NI = (QB * T::KP + NT - 1) / NT, RS = K <= 12 ? 4 : 8;  // steps per round
+  constexpr int QB = 64, NI = (QB * T::KP + NT - 1) / NT;  // (RS: 4-row steps per round)
   const int cg = ig * NW + wv;
   const bool cgv = cg < T::NCG;
   const int cell = 4 * (4 * (cgv ? cg : 0) + blk) + lo;
@@ -718,9 +718,10 @@ struct FT {
   static constexpr int RE_CAP = TWO ? 6 : 12;
   static constexpr int WPE = TWO ? 4 : 1;
   static constexpr int YU = 8;                  // Y entries in flight per thread
-  // partial rows of one (gene, cell) entry loaded together per fill round (balanced plans give a
-  // gene about 2.4 rows per rating at K = 30; rows past these are summed one dependent load at a time)
-  static constexpr int RW = MMSBM_GENE_RW ? MMSBM_GENE_RW : TWO ? 2 : 4;
+  // partial rows of one (gene, cell) entry loaded together per fill round; rows past these are
+  // summed one dependent load at a time (4 measured the same as 2 at K=30, 1,923.6 vs 1,924.9 us,
+  // profiles/r04s_large_ab.txt, and spills at K = 24)
+  static constexpr int RW = MMSBM_GENE_RW ? MMSBM_GENE_RW : 2;
   static_assert(NXG * KSPLIT == 8, "gene part: one (a group, k part) per wave");
   static_assert(NGW * K <= NT, "gene part epilogue: one (gene, a) per thread");
   static_assert(LDS <= 160 * 1024, "gene kernel LDS over budget");
@@ -734,7 +735,8 @@ template <int K>
 __device__ __forceinline__ void x0_tiles(const double* __restrict__ Mg, const double* __restrict__ p,
                                          int a, int hi, int kb, int ke, double (&acc)[FT<K>::GT]) {
   using F = FT<K>;
-  constexpr int K2 = K * K, UB = 8, GT = F::GT;
+  // (UB k-steps per batch; two batches in flight: 4 under the 128-VGPR budget of K = 20-23)
+  constexpr int K2 = K * K, UB = F::TWO ? 4 : 8, GT = F::GT;
   const int ac = a < K ? a : K - 1;
   // batches of UB k-steps, double-buffered: the next batch's p loads (L2) are in flight during
   // this batch's MFMAs (a batch past ke loads clamped addresses and is not used)
@@ -950,11 +952,40 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
     const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
     const int sw = sa, sp = sw / T::NIG, ig = sw % T::NIG;
     const int* d = sp_desc + 3 * sp;
-    s_partial<K>(theta + (size_t)b * P * K, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
-                 spart + ((size_t)b * n_sp + sp) * T::K3, Ms, ig, tid, wv, hi, blk, lo, st_);
+    s_partial<K, FT<K>::TWO ? 4 : 8>(theta + (size_t)b * P * K, prows + (size_t)b * n_prows * T::K2, prow_gene,
+                                     d[1], d[2], spart + ((size_t)b * n_sp + sp) * T::K3, Ms, ig, tid, wv, hi,
+                                     blk, lo, st_);
     st_.flush(3, ((long long)b * gridDim.x + w) * NW + wv, lane);
   } else {
     const long long item = ya * FT<K>::NT + tid;
+    genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
+  }
+}
+
+// The S and Y workgroups as a launch of their own, after the gene (x0) workgroups' launch
+// (mmsbm_ctx::gsplit): they need 16 KB of LDS (s_partial's theta staging) or none, and at most
+// 128 VGPRs, so four of them share a CU, where inside gene_kernel they inherit its LDS (150 KB at
+// K = 30) and VGPR budget and run one per CU.
+template <int K>
+__global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(4))) void gene_sy_kernel(
+    const double* __restrict__ theta, const double* __restrict__ prows, const int* __restrict__ prow_gene,
+    const int* __restrict__ sp_desc, const double* __restrict__ ybuf, const int* __restrict__ yptr,
+    double* __restrict__ ysum, double* __restrict__ spart, int P, long long n_prows, long long n_y, int n_sp,
+    int n_sp_wg) {
+  using T = KT<K>;
+  extern __shared__ __attribute__((aligned(16))) double Ms[];
+  const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
+  Stamp st_{};
+  if (w < n_sp_wg) {
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
+    const int sp = w / T::NIG, ig = w % T::NIG;
+    const int* d = sp_desc + 3 * sp;
+    s_partial<K, 8>(theta + (size_t)b * P * K, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
+                    spart + ((size_t)b * n_sp + sp) * T::K3, Ms, ig, tid, wv, hi, blk, lo, st_);
+  } else {
+    const long long item = (long long)(w - n_sp_wg) * FT<K>::NT + tid;
     genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
   }
 }
@@ -1267,6 +1298,9 @@ struct mmsbm_ctx {
   // (K=30 gene 1,930 vs 1,928 us; K=20 x 8 128 vs 113 us, profiles/r04r_ysplit_ab.txt) — the gene
   // kernel's waves leave a CU no VGPRs for the Y waves
   bool ysplit = false;
+  // large-K gene kernel as two launches: x0 workgroups, then S + Y workgroups (gene_sy_kernel) at
+  // their own LDS and VGPR budget; MMSBM_GSPLIT=0: one launch (measurement)
+  bool gsplit = true;
   hipStream_t ys = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   const double *g_theta = nullptr, *g_pr = nullptr;
@@ -1377,9 +1411,23 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
       ysum_kernel<K><<<dim3((unsigned)nyb, c->B), 256, 0, c->ys>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
       HIP_TRY(hipGetLastError());
     }
-    gene_kernel<K><<<dim3(ngw + nspw + nyw, c->B), F::NT, F::LDS, s>>>(
-        theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
-        c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, nspw);
+    // two launches where gene_kernel runs one workgroup per CU (K >= 24: K=30 gene 1,867 -> 1,850
+    // us); at K = 20-23 two gene workgroups share a CU and the single launch, whose S and Y
+    // workgroups overlap the x0 ones, is faster (K=20 x 8: 129.5 vs 154.7 us,
+    // profiles/r04v_gsplit_ab.txt)
+    if (c->gsplit && !F::TWO) {  // x0 workgroups, then the S and Y workgroups at their own budget
+      gene_kernel<K><<<dim3(ngw, c->B), F::NT, F::LDS, s>>>(
+          theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
+          c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, 0);
+      HIP_TRY(hipGetLastError());
+      gene_sy_kernel<K><<<dim3(nspw + nyw, c->B), F::NT, F::LDS_SP * 8, s>>>(
+          theta, c->prows, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx + pk, c->spart, c->P, h.n_prows,
+          h.n_y, std::max(h.n_sp, 1), nspw);
+    } else {
+      gene_kernel<K><<<dim3(ngw + nspw + nyw, c->B), F::NT, F::LDS, s>>>(
+          theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
+          c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, nspw);
+    }
     if (c->ysplit) {
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(c->ev_join, c->ys));
@@ -1636,6 +1684,7 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   c->device = device;
   if (const char* gi = getenv("MMSBM_GRAPH")) c->graph_iters = std::max(0, atoi(gi));
   if (const char* ysp = getenv("MMSBM_YSPLIT")) c->ysplit = ysp[0] != '0';
+  if (const char* gsp = getenv("MMSBM_GSPLIT")) c->gsplit = gsp[0] != '0';
   if (MMSBM_STAMP && getenv("MMSBM_STAMP")) {
     DeviceGuard g(device);
     const size_t bytes = sizeof(unsigned long long) * 5 * STAMP_WAVES * STAMP_SLOTS;
