@@ -113,6 +113,9 @@ constexpr int y_stride(int K) { return (K + MMSBM_YALIGN - 1) / MMSBM_YALIGN * M
 #endif
 constexpr int PASS_WPE = MMSBM_PASS_WPE;
 
+#ifndef MMSBM_GENE_GT24
+#define MMSBM_GENE_GT24 0
+#endif
 // gene_kernel fill rounds: partial rows per entry loaded together (0 = FT's choice; measurement)
 #ifndef MMSBM_GENE_RW
 #define MMSBM_GENE_RW 0
@@ -699,7 +702,9 @@ struct FT {
   static constexpr int KS = (K2 + 3) / 4;       // k-steps over the dense (b, h) cells
   static constexpr int K2P = 4 * KS;
   static constexpr int NXG = (NG + 3) / 4;      // MFMA groups of 4 a tiles
-  static constexpr int GT = 4;                  // gene row tiles per workgroup
+  // gene row tiles per workgroup: 4 (16 genes); -DMMSBM_GENE_GT24=1 takes 2 (8 genes) from K = 24,
+  // so two gene workgroups share a CU (measurement)
+  static constexpr int GT = (MMSBM_GENE_GT24 && K >= 24) ? 2 : 4;
   static constexpr int NGW = 4 * GT;            // genes per workgroup
   static constexpr int NT = 512;
   static constexpr int KSPLIT = 8 / NXG;        // k-step parts over the 8 waves
@@ -1411,11 +1416,10 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
       ysum_kernel<K><<<dim3((unsigned)nyb, c->B), 256, 0, c->ys>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
       HIP_TRY(hipGetLastError());
     }
-    // two launches where gene_kernel runs one workgroup per CU (K >= 24: K=30 gene 1,867 -> 1,850
-    // us); at K = 20-23 two gene workgroups share a CU and the single launch, whose S and Y
-    // workgroups overlap the x0 ones, is faster (K=20 x 8: 129.5 vs 154.7 us,
-    // profiles/r04v_gsplit_ab.txt)
-    if (c->gsplit && !F::TWO) {  // x0 workgroups, then the S and Y workgroups at their own budget
+    // two launches from K = 24 (K=30 gene 1,778 -> 1,745 us, profiles/r04w_gsplit_ab.txt); at
+    // K = 20-23 two gene workgroups share a CU and the single launch, whose S and Y workgroups
+    // overlap the x0 ones, is faster (K=20 x 8: 129.5 vs 154.7 us, profiles/r04v_gsplit_ab.txt)
+    if (c->gsplit && K >= 24) {  // x0 workgroups, then the S and Y workgroups at their own budget
       gene_kernel<K><<<dim3(ngw, c->B), F::NT, F::LDS, s>>>(
           theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
           c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, 0);

@@ -44,9 +44,6 @@ enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
 #ifndef MMSBM_SK_PVS
 #define MMSBM_SK_PVS 1  // P^s rows at an odd stride (0: K^2, round 3), see SKT::PVS
 #endif
-#ifndef MMSBM_SK_SCOOP_IL
-#define MMSBM_SK_SCOOP_IL 1  // the S scoop's stretch order per step, see sk_scoop_row
-#endif
 #ifndef MMSBM_SK_GHOIST
 #define MMSBM_SK_GHOIST 0  // 1: the first block's theta gathers before the V tables (after the barrier)
 #endif
@@ -95,20 +92,6 @@ struct SKT {
                 "V reads past the wave's slots and records");
   static_assert(16 * NCG <= SLOT + SK_ROWS + THL, "S operand reads past the slots and records");
 };
-
-// Stretch slot (of its wave) of MFMA row k = hi in S-scoop step qs.  The B operand reads M rows
-// qt at stride SLOT, and a ds_read_b64 lane group (32 lanes) holds rows hi = 0, 1 (2, 3): with
-// GUK = 8 and 4 SLOT = 16 (mod 32) doubles (K = 9, 10: SLOT 84, 100) the steps take slots
-// {0, 4, 1, 5} then {2, 6, 3, 7}, so the two rows of a group sit 4 SLOT apart, 32 banks, instead of
-// SLOT (4 or 20 (mod 32): half the group's lanes on shared banks).  The order in which the S
-// partial sums its rows changes with it (fixed either way).
-template <int GUK, int SLOT>
-__device__ __forceinline__ int sk_scoop_row(int qs, int hi) {
-  if constexpr (MMSBM_SK_SCOOP_IL && GUK == 8 && (4 * SLOT) % 32 == 16)
-    return 2 * (qs & 1) + (hi >> 1) + 4 * (hi & 1);
-  else
-    return (4 * qs) % GUK + hi;
-}
 
 // n / d by v_rcp_f64 and two Newton steps plus a residual correction (within an ulp or two of the
 // IEEE quotient; d > 0 here): a shorter dependent chain than the IEEE division's scale / fixup
@@ -526,8 +509,8 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
 #if MMSBM_SK_SCOOP
   if (MODE == SK_A || (MODE == SK_U && s == 0)) {  // (workgroup-uniform)
     // ---- the workgroup's S partial in one pass over all its stretches: S_r[a][cell] =
-    // sum_q theta_{g_q}[a] M_q[cell] over the rows q of every wave, wave by wave, slots in
-    // sk_scoop_row order (m = a, k = q, n = cell; A from the waves' pivot theta rows, B from their M rows).  Rows of
+    // sum_q theta_{g_q}[a] M_q[cell] over the rows q = (wave, slot) of every wave, in that order
+    // (m = a, k = q, n = cell; A from the waves' pivot theta rows, B from their M rows).  Rows of
     // absent stretches are zero (V zeros, zero theta); an empty slot zeroes its own first.  One
     // barrier, then each wave takes (a tile, cell group) items and stores its cells directly.
     constexpr int WV = MODE == SK_U ? T::WAVE_U : T::WAVE;
@@ -547,7 +530,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     for (int j = 0; j < NIW; ++j) acc[j] = 0.0;
 #pragma unroll 4
     for (int qs = 0; qs < QS; ++qs) {
-      const int qw = (4 * qs) / GUK, qt = sk_scoop_row<GUK, SLOT>(qs, hi);  // (wave qw uniform per step)
+      const int qw = (4 * qs) / GUK, qt = (4 * qs) % GUK + hi;  // (wave qw uniform per step)
       const double* __restrict__ wq = smem + T::PSD + qw * WV;
       const double* __restrict__ thq = wq + GUK * SLOT + SK_ROWS + qt * 4 * NG + lo;
       const double* __restrict__ mq = wq + qt * SLOT + 4 * blk + lo;
@@ -926,7 +909,7 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
     for (int j = 0; j < NIW; ++j) acc[j] = 0.0;
 #pragma unroll 4
     for (int qs = 0; qs < QS; ++qs) {
-      const int qw = (4 * qs) / GUK, qt = sk_scoop_row<GUK, SLOT>(qs, hi);
+      const int qw = (4 * qs) / GUK, qt = (4 * qs) % GUK + hi;
       const double* __restrict__ wq = smem + T::PSD + qw * Y::WAVE;
       const double* __restrict__ thq = wq + GUK * SLOT + SK_ROWS + qt * 4 * NG + lo;
       const double* __restrict__ mq = wq + qt * SLOT + 4 * blk + lo;
