@@ -239,11 +239,13 @@ int main() {
   const bool small = gcap <= 0, fill = gcap == -1 || gcap == -2 || gcap == -4, yent = gcap == -4;
   // PLAN_NO_BALANCE=1: the large-K units packed whole-run-wise (round 3, MMSBM_BALANCE=0)
   const bool balance = !getenv("PLAN_NO_BALANCE");
+  // PLAN_MERGE=1: one partial row per (workgroup, gene) (the K >= 25 pass kernel merges its waves' parts)
+  const bool merge = getenv("PLAN_MERGE") != nullptr;
   const int gu = (gcap == 0 || gcap == -2) ? 4 : 8;
   const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill, gu,
                                 85, yent)
                         : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows, false, 1024,
-                                false, GU, 85, false, balance);
+                                false, GU, 85, false, balance, merge);
   if (fill) {  // every unit but the last of its (stream, rating) section is full: LCAP_SK chunks or GU stretches
     for (long long u = 0; u + 1 < pl.n_units; ++u) {
       const int* d = &pl.udesc[(size_t)u * UD];
@@ -358,6 +360,25 @@ int main() {
           if (pl.prow_gene[q] != g) return fail("prow_ptr gene", q, g);
       }
     }
+
+  // 4b. merged plans: a partial row's chunks lie in one workgroup, and inside a workgroup a gene's
+  //     chunks share one row
+  if (merge != pl.merge || (merge && !balance)) return fail("merge flag", pl.merge);
+  if (pl.merge) {
+    std::vector<int> prow_wg(pl.n_prows, -1);
+    for (int w = 0; w < n_wg; ++w) {
+      const int c0 = pl.wg_units[w * (NW + 1)], c1 = pl.wg_units[w * (NW + 1) + NW];
+      for (int c = c0; c < c1; ++c) {
+        const int q = pl.chunk_prow[c];
+        if (prow_wg[q] >= 0 && prow_wg[q] != w) return fail("merged row spans workgroups", q, w);
+        prow_wg[q] = w;
+        if (c > c0) {
+          const bool same = pl.rows[(long long)c * CH].x == pl.rows[(long long)(c - 1) * CH].x;
+          if (same != (q == pl.chunk_prow[c - 1])) return fail("merged row per gene", c, q);
+        }
+      }
+    }
+  }
 
   // 5. S-partial descriptors tile each rating's stream-0 partial rows
   for (int r = 0; r < R; ++r) {

@@ -94,6 +94,18 @@ def test_plan_invariants_unbalanced(plan_check, P, E, units, gcap, sp_rows, hub)
     _check(plan_check, P, E, units, gcap, sp_rows, hub, env={"PLAN_NO_BALANCE": "1"})
 
 
+# merged partial rows (K >= 25 plans): one per (workgroup, gene), fewer than one per unit stretch
+@pytest.mark.parametrize("P,E,units,gcap,sp_rows,hub", [
+    (500, 40000, (64, 64), 13, 120, 0.0),
+    (300, 5000, (1536, 3072), 13, 120, 30.0),
+    (40, 600, (1, 1), 13, 16, 0.0),
+])
+def test_plan_invariants_merged(plan_check, P, E, units, gcap, sp_rows, hub):
+    merged = _check(plan_check, P, E, units, gcap, sp_rows, hub, env={"PLAN_MERGE": "1"})
+    plain = _check(plan_check, P, E, units, gcap, sp_rows, hub)
+    assert int(merged[4]) <= int(plain[4])  # partial rows
+
+
 def test_balanced_plan_fewer_workgroups(plan_check):
     # K=30-like: 5 genes per workgroup, runs of ~10 chunks, 64-chunk units: the round-3 plan's
     # units took whole runs up to 64 chunks, so a workgroup's gene cap left most of its 8 units

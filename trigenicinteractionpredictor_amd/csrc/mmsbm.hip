@@ -354,7 +354,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
     const int* __restrict__ wg_code, const int* __restrict__ wg_gene, const int* __restrict__ vgenes,
     const double* __restrict__ theta, const double* __restrict__ pr, double* __restrict__ ybuf,
     double* __restrict__ prows, double* __restrict__ partL, int P, int R, long long n_y,
-    long long n_prows, int n_wg, double eps, int gcap) {
+    long long n_prows, int n_wg, double eps, int gcap, int merge) {
   using T = KT<K>;
   constexpr int NG = T::NG, TR = T::TR, VR = T::VR;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -398,6 +398,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   auto ld_rec = [&](int q) -> int { return rbase[(size_t)q * rstride]; };
   auto clampq = [&](int q) { return q < c1 ? q : c1 - 1; };
   const bool any = c0 < c1;
+  // Merged partial rows (Plan::merge, K >= MMSBM_LDS_BIG, where one workgroup runs per CU and the
+  // registers are there): one row per (workgroup, gene).  A wave's first stretch may continue the
+  // previous wave's run (first_cont: its M goes to the workgroup's LDS after the chunk loops) and
+  // its last may be continued by the next waves (last_cont: it adds their parts, in wave order,
+  // before the one store).
+  constexpr bool MG = EM && K >= MMSBM_LDS_BIG;
+  bool first_cont = false, last_cont = false;
+  if (MG && merge && any) {
+    const int wc0 = wg_units[w * (NW + 1)], wc1 = wg_units[w * (NW + 1) + NW];
+    first_cont = c0 > wc0 && __builtin_amdgcn_readfirstlane(chunk_prow[c0 - 1]) ==
+                                 __builtin_amdgcn_readfirstlane(chunk_prow[c0]);
+    last_cont = c1 < wc1 && __builtin_amdgcn_readfirstlane(chunk_prow[c1]) ==
+                                __builtin_amdgcn_readfirstlane(chunk_prow[c1 - 1]);
+  }
   int rv[U];
 #pragma unroll
   for (int i = 0; i < U - 1; ++i) rv[i] = any ? ld_rec(clampq(c0 + i)) : 0;
@@ -538,6 +552,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   d4v m16[NX16 * NX16];
 #pragma unroll
   for (int t = 0; t < NX16 * NX16; ++t) m16[t] = d4v{0.0, 0.0, 0.0, 0.0};
+  d4v mc[MG ? NX16 * NX16 : 1];  // MG: the first stretch's M when it continues a run
+#pragma unroll
+  for (int t = 0; t < (MG ? NX16 * NX16 : 1); ++t) mc[t] = d4v{0.0, 0.0, 0.0, 0.0};
+  bool first_st = true, kept = false;  // kept: the last stretch heads a merged row
   double ll = 0.0;
   // the image's pad columns are read (times a zero Z entry) by the d dot product and are the Z'
   // operand's k >= K rows: keep them 0
@@ -636,18 +654,30 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
             for (int ty = 0; ty < NX16; ++ty)
               m16[tx * NX16 + ty] = mfma16(a16[tx], b16[ty], m16[tx * NX16 + ty]);
           if (q + 1 >= c1 || pr1 != pr0) {  // end of this gene stretch: its partial row
-            double* __restrict__ out = pb + (size_t)pr0 * T::K2;
+            const bool to_mc = MG && first_st && first_cont;       // (uniform)
+            const bool keep = MG && !to_mc && q + 1 >= c1 && last_cont;
+            first_st = false;
+            kept = keep;
+            if (to_mc) {
 #pragma unroll
-            for (int tx = 0; tx < NX16; ++tx)
+              for (int t = 0; t < NX16 * NX16; ++t) {
+                mc[MG ? t : 0] = m16[t];
+                m16[t] = d4v{0.0, 0.0, 0.0, 0.0};
+              }
+            } else if (!keep) {  // (keep: the loop ends here, m16 stays for the merge)
+              double* __restrict__ out = pb + (size_t)pr0 * T::K2;
 #pragma unroll
-              for (int ty = 0; ty < NX16; ++ty)
+              for (int tx = 0; tx < NX16; ++tx)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                  const int x = 16 * tx + hi + 4 * i, y = 16 * ty + col;
-                  if (x < K && y < K && !(MMSBM_ABL & 4)) st_wt(out + x * K + y, m16[tx * NX16 + ty][i]);
-                  else if (MMSBM_ABL & 4) ll += m16[tx * NX16 + ty][i];
-                  m16[tx * NX16 + ty][i] = 0.0;
-                }
+                for (int ty = 0; ty < NX16; ++ty)
+#pragma unroll
+                  for (int i = 0; i < 4; ++i) {
+                    const int x = 16 * tx + hi + 4 * i, y = 16 * ty + col;
+                    if (x < K && y < K && !(MMSBM_ABL & 4)) st_wt(out + x * K + y, m16[tx * NX16 + ty][i]);
+                    else if (MMSBM_ABL & 4) ll += m16[tx * NX16 + ty][i];
+                    m16[tx * NX16 + ty][i] = 0.0;
+                  }
+            }
           }
         }
         // next chunk's image into the other buffer (its reads of this buffer are done)
@@ -657,6 +687,54 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
     }
   }
   st_.mark(2);
+  if constexpr (MG) {
+    if (merge) {  // (workgroup-uniform) the V tables and images are dead: NW slots of K^2 words
+      static_assert((4 * T::VDBL + T::tg_dbl(4)) * 8 + T::IMG_BYTES >= NW * T::K2 * 8,
+                    "merge slots within the smallest gene cap's LDS");
+      const int col = lane & 15;
+      __syncthreads();
+      if (first_cont) {
+#pragma unroll
+        for (int tx = 0; tx < NX16; ++tx)
+#pragma unroll
+          for (int ty = 0; ty < NX16; ++ty)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int x = 16 * tx + hi + 4 * i, y = 16 * ty + col;
+              if (x < K && y < K) smem[wv * T::K2 + x * K + y] = mc[tx * NX16 + ty][i];
+            }
+      }
+      __syncthreads();
+      if (kept) {
+        const int mypr = __builtin_amdgcn_readfirstlane(chunk_prow[c1 - 1]);
+        for (int nx = wv + 1; nx < NW; ++nx) {  // the continuing waves, in order
+          const int n0 = wg_units[w * (NW + 1) + nx], n1 = wg_units[w * (NW + 1) + nx + 1];
+          if (n0 == n1) continue;  // (an empty unit)
+          if (__builtin_amdgcn_readfirstlane(chunk_prow[n0]) != mypr) break;
+#pragma unroll
+          for (int tx = 0; tx < NX16; ++tx)
+#pragma unroll
+            for (int ty = 0; ty < NX16; ++ty)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int x = 16 * tx + hi + 4 * i, y = 16 * ty + col;
+                if (x < K && y < K) m16[tx * NX16 + ty][i] += smem[nx * T::K2 + x * K + y];
+              }
+          if (__builtin_amdgcn_readfirstlane(chunk_prow[n1 - 1]) != mypr) break;
+        }
+        double* __restrict__ out = pb + (size_t)mypr * T::K2;
+#pragma unroll
+        for (int tx = 0; tx < NX16; ++tx)
+#pragma unroll
+          for (int ty = 0; ty < NX16; ++ty)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int x = 16 * tx + hi + 4 * i, y = 16 * ty + col;
+              if (x < K && y < K) st_wt(out + x * K + y, m16[tx * NX16 + ty][i]);
+            }
+      }
+    }
+  }
   if constexpr (MMSBM_ABL != 0 && EM)  // ablation builds: keep the skipped stores' values live
     if (ll == -1.2345e300) partL[0] = ll;
   st_.t[5] = (unsigned long long)(c1 - c0);
@@ -1445,12 +1523,13 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
       if ((rc = lds_opt_in(c, 0, &pass_kernel<K, PASS_A>, T::LDS_A))) return rc;
       pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.row_y, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
-          theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, h.n_y, h.n_prows, h.n_wg_a, c->eps, c->gcap);
+          theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, h.n_y, h.n_prows, h.n_wg_a, c->eps, c->gcap,
+          h.merge ? 1 : 0);
     } else {
       if ((rc = lds_opt_in(c, 1, &pass_kernel<K, PASS_LL>, T::LDS_A))) return rc;
       pass_kernel<K, PASS_LL><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, nullptr, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
-          theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, 0, h.n_prows, h.n_wg_a, c->eps, c->gcap);
+          theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, 0, h.n_prows, h.n_wg_a, c->eps, c->gcap, 0);
     }
   }
   HIP_TRY(hipGetLastError());
@@ -1838,13 +1917,17 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   // runs per unit as in round 3 (measurement)
   const char* bal = getenv("MMSBM_BALANCE");
   const bool balance = !(bal && bal[0] == '0');
+  // one partial row per (workgroup, gene) where the pass kernel merges its waves' parts (K >=
+  // MMSBM_LDS_BIG); MMSBM_MERGE=0: one per unit stretch (measurement)
+  const char* mg = getenv("MMSBM_MERGE");
+  const bool merge = !c->sk && c->K >= MMSBM_LDS_BIG && !(mg && mg[0] == '0');
   // stream-0 partial rows per S partial at large K (each S partial is K^3 words the update sums);
   // MMSBM_SP_ROWS=n overrides it (measurement)
   int sp_rows = c->K <= 12 ? 16 : 4 * c->K;
   if (const char* e = getenv("MMSBM_SP_ROWS")) sp_rows = std::max(4, atoi(e));
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
                            c->gcap, sp_rows, c->sk, 1024, c->sk_fused,
-                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance);
+                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge);
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
   sd.unit_target = c->sk_fused ? units_a : 0;

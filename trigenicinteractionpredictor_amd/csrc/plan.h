@@ -84,6 +84,7 @@ struct Plan {
   // rating) in one range, (stream, rating, row) order inside: fin sums one range per gene)
   std::vector<int> prow_g;         // [n_prows] gene-major position of each partial row
   std::vector<int> gptr;           // [P + 1] each gene's range of gene-major positions
+  bool merge = false;              // large-K: one partial row per (workgroup, gene) (see build)
   int rounds_a = 1, rounds_b = 1;  // unit rounds per workgroup (stream 0 / streams 1, 2)
   long long n_units = 0;
   // slot layout the small-K kernels read (make_slots below); group 0 = stream 0 (pass A), group 1 =
@@ -259,8 +260,9 @@ inline void make_slots(Plan& pl) {
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
                   int wg_target = 1024, bool fill = false, int gu = GU, int rho_pct = 85,
-                  bool yent = false, bool balance = true) {
+                  bool yent = false, bool balance = true, bool merge = false) {
   Plan pl;
+  pl.merge = merge && balance && !small && em;
   pl.gu = std::max(1, std::min(gu, GU));
   pl.R = R;
   pl.P = P;
@@ -458,14 +460,17 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
         }
       }
       if (s != 0) pl.chunk_vslot.resize(pl.chunk_vslot.size() + nch, 0);
-      // partial rows: a new one at every unit start and every gene change inside a unit
+      // partial rows: a new one at every unit start and every gene change inside a unit; with
+      // `merge` (balanced large-K plans) at every workgroup start and gene change: the waves that
+      // share a gene's run add their parts in the workgroup (pass kernel) before one store
       if (em) {
         int* ptr = &pl.prow_ptr[((size_t)s * R + r) * (P + 1)];
         const long long first_prow = pl.n_prows;
         int u = 0;
         for (int c = 0; c < nch; ++c) {
           while (u + 1 < (int)ub.size() && ub[u + 1] <= c) ++u;
-          if (c == ub[u] || cgene[c] != cgene[c - 1]) {
+          const int start = (bal && merge) ? ub[(u / NW) * NW] : ub[u];
+          if (c == start || cgene[c] != cgene[c - 1]) {
             pl.prow_gene.push_back(cgene[c]);
             ++pl.n_prows;
           }
