@@ -158,6 +158,35 @@ def test_work_plan_splits_match_oracle(tmp_path, monkeypatch, K, units):
     np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
 
 
+@pytest.mark.parametrize("K,P,E,env", [
+    (28, 40, 3000, {}),                        # balanced units + merged rows: runs span waves
+    (28, 40, 3000, {"MMSBM_UNITS": "1,1"}),    # 64-chunk units: runs span 3+ waves of a workgroup
+    (30, 60, 4000, {"MMSBM_MERGE": "0"}),      # one row per unit stretch (measurement path)
+    (30, 60, 4000, {"MMSBM_BALANCE": "0"}),    # whole runs per unit (round-3 packing)
+    (26, 50, 3000, {"MMSBM_GSPLIT": "0"}),     # the gene kernel in one launch
+    (20, 60, 4000, {"MMSBM_UNITS": "1,1"}),    # balanced without merging (K < 25)
+])
+def test_large_k_plan_variants_match_oracle(tmp_path, monkeypatch, K, P, E, env):
+    """The round-4 large-K work plans (csrc/plan.h pack_balanced, Plan::merge; mmsbm.hip's merged
+    partial rows and split gene launch) with few genes and long pivot runs, so a run's chunks
+    spread over several waves of a workgroup, vs the C oracle after 2 iterations."""
+    for k in ("MMSBM_UNITS", "MMSBM_MERGE", "MMSBM_BALANCE", "MMSBM_GSPLIT"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tr, te = _fold(tmp_path, P, E, seed=K + 7, multi_frac=0.05, both_frac=0.02)
+    m = _gpu_model(tr, te)
+    random.seed(K + 3)
+    m.initialize_parameters(K)
+    theta0, pr0 = np.array(m.theta), np.array(m.pr)
+    m.make_iterations(2)
+    th_o, pr_o, L_o, LT_o = _oracle_run(m, theta0, pr0, 2)
+    np.testing.assert_allclose(np.array(m.theta), th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
+    np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
+
+
 @pytest.mark.parametrize("K,P,E", [(30, 3000, 4000), (12, 4000, 3000), (4, 30, 1500), (32, 40, 900)])
 def test_short_and_long_pivot_runs_match_oracle(tmp_path, K, P, E):
     """Many genes with one or two observations each (every chunk a new pivot gene: stream-0
