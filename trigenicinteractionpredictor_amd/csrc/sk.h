@@ -391,14 +391,17 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
 #pragma unroll
         for (int q = 0; q < LC; ++q) {
           if (q < nb) {
-#if MMSBM_SK_TRSWZ  // column swizzle c ^ 4 (o >> 1): the reads of observations 0 / 2 (1 / 3) hit
-                    // different banks
-            TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = gv[q];
+#if MMSBM_SK_TRSWZ  // column swizzle c ^ 4 o (o = the observation row): the compiler pairs the
+                    // reads of hs = 0, 2 into ds_read2_b64, whose 16-lane groups bank on (a/4) mod
+                    // 32, where the 4 rows (16 doubles apart) coincide; c ^ 4 o moves each row to
+                    // its own 8 banks (round 3's c ^ 4 (o >> 1) left rows 0 / 1 and 2 / 3 sharing:
+                    // 56 % of the kernel's LDS conflict cycles, profiles/r05h_lds_attribution.txt)
+            TRl[16 * hi + (col ^ (4 * hi))] = gv[q];
             wave_lds_sync();
             double z = 0.0;
 #pragma unroll
             for (int hs = 0; hs < NG; ++hs)
-              z = mfma4(TRl[16 * lo + ((4 * hs + hi) ^ (4 * (lo >> 1)))], vb[hs], z);
+              z = mfma4(TRl[16 * lo + ((4 * hs + hi) ^ (4 * lo))], vb[hs], z);
 #else
             TRl[lane] = gv[q];
             wave_lds_sync();
@@ -829,19 +832,19 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
 #pragma unroll
       for (int q = 0; q < LC; ++q) {
         if (q < nb) {
-          TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = gv[q];
+          TRl[16 * hi + (col ^ (4 * hi))] = gv[q];
           wave_lds_sync();
           double z = 0.0;
 #pragma unroll
           for (int hs = 0; hs < NG; ++hs)
-            z = mfma4(TRl[16 * lo + ((4 * hs + hi) ^ (4 * (lo >> 1)))], vb[hs], z);
+            z = mfma4(TRl[16 * lo + ((4 * hs + hi) ^ (4 * lo))], vb[hs], z);
           // (a wave's LDS accesses execute in order: the reads above precede this write)
-          TRl[16 * hi + (col ^ (4 * (hi >> 1)))] = kcol ? ga[q] : 0.0;
+          TRl[16 * hi + (col ^ (4 * hi))] = kcol ? ga[q] : 0.0;
           wave_lds_sync();
           double zp = 0.0;
 #pragma unroll
           for (int bs = 0; bs < NG; ++bs)
-            zp = mfma4(TRl[16 * lo + ((4 * bs + hi) ^ (4 * (lo >> 1)))], vbt[bs], zp);
+            zp = mfma4(TRl[16 * lo + ((4 * bs + hi) ^ (4 * lo))], vbt[bs], zp);
           // the count of observation hi of this chunk (lane 4 q + hi's record), by scalar reads
           const int n0 = __builtin_amdgcn_readlane(wlane, 4 * q), n1 = __builtin_amdgcn_readlane(wlane, 4 * q + 1);
           const int n2 = __builtin_amdgcn_readlane(wlane, 4 * q + 2), n3 = __builtin_amdgcn_readlane(wlane, 4 * q + 3);
