@@ -86,33 +86,11 @@ def parse():
 def spawn_ranks(n):
     """`--gpus N` without a launcher: start N copies of this script, one rank per GPU (RANK,
     LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT as torch.distributed.run sets them), BEFORE this
-    process touches any GPU, and return the worst exit code.  Rank 0 prints the JSON line.
+    process touches any GPU, and return the first failure's exit code (a failed rank has the
+    others terminated: they would wait in a barrier).  Rank 0 prints the JSON line.
     (The reference scales the same way, one OS process per batch of samples: src/run.sh:36-45.)"""
-    import socket
-    import subprocess
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env))
-    rc = 0
-    alive = list(procs)
-    while alive:
-        for p in list(alive):
-            code = p.poll()
-            if code is None:
-                continue
-            alive.remove(p)
-            if code != 0:
-                rc = rc or (code if code > 0 else 128 - code)
-                for q in alive:            # a failed rank would leave the others in a barrier
-                    q.terminate()
-        time.sleep(0.05)
-    return rc
+    from trigenicinteractionpredictor_amd.launch import spawn_ranks as spawn
+    return spawn([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], n)
 
 
 KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, Z', d, c, the j / k Y entries, M0 "
@@ -240,6 +218,8 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
     head = tf if credited else exe_tf
     return {"bound": "mfma", "achieved": head, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": head / FP64_PEAK_TFLOPS,
+            "frac_credited": tf / FP64_PEAK_TFLOPS,
+            "frac_executed": exe_tf / FP64_PEAK_TFLOPS,
             "frac_basis": ("SURVEY 8d credited FLOPs" if credited else
                            "executed FLOPs (the 8d credit exceeds the FP64 peak)"),
             "credited": {"achieved": tf, "frac": tf / FP64_PEAK_TFLOPS},
@@ -384,6 +364,12 @@ def main():
     if args.launch_check:
         launch_check(args, world, rank)
         return 0
+    if args.backend == "nccl" and world > 1:
+        from trigenicinteractionpredictor_amd.launch import visible_gpus
+        if world > visible_gpus():   # RCCL: one GPU per rank of a communicator
+            print("bench.py: %d nccl ranks need %d GPUs, %d visible" % (world, world, visible_gpus()),
+                  file=sys.stderr)
+            return 2
     train, test = make_fold(args.P, args.E, rank, args.hub, args.test_frac)
     cpu_rec = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -426,11 +412,14 @@ def main():
     # restart sharding: global sample s = rank*B + b; one RNG stream seeded once, like :1149/:1260.
     # link sharding: every rank holds the same B samples (s = 0..B-1) and 1/world of the links.
     first = 0 if links_mode else rank * B
-    from trigenicinteractionpredictor_amd.restarts import (gather_rows, init_samples, replay_check,
-                                                           result_rows, rows_digest)
+    from trigenicinteractionpredictor_amd.restarts import (family_for_batch, gather_rows, init_samples,
+                                                           replay_check, result_rows, rows_digest)
     sample_ids = list(range(first, first + B))
     thetas, prs = init_samples(host, K, sample_ids, args.seed)
-    eng = EMEngine(K, host.P, B=B, device=dev)
+    # the small-K kernel family follows the configured samples per GPU (SK_U for one, SK_Y from
+    # two; include/mmsbm.h mmsbm_set_family), and the replay below uses the same family
+    family = family_for_batch(B)
+    eng = EMEngine(K, host.P, B=B, device=dev, family=family)
     ids, counts = host._link_arrays(0)           # the native reader's arrays (links order)
     tids, tcounts = host._link_arrays(1)
     if links_mode:
@@ -482,10 +471,10 @@ def main():
     n_gathered = int(rows.shape[0])
     scale_check = None
     if rank == 0 and dist_on and not links_mode:
-        # every sample replayed as ONE batch on this GPU: a sample's bits do not depend on its
-        # batch or rank, so the gathered values must equal the replay bit for bit
+        # every sample replayed as ONE batch on this GPU: within one kernel family a sample's bits
+        # do not depend on its batch or rank, so the gathered values must equal the replay bit for bit
         def factory(nb):
-            e = EMEngine(K, host.P, B=nb, device=dev)
+            e = EMEngine(K, host.P, B=nb, device=dev, family=family)
             e.set_links(0, ids, counts)
             e.set_links(1, tids, tcounts)
             return e
@@ -529,6 +518,10 @@ def main():
                         "replay_check": scale_check},
             "build_id": build_id,
             "roofline": roofline,
+            # both bases of the roofline fraction, whichever `roofline.frac` reports
+            "frac_credited": roofline["frac_credited"],
+            "frac_executed": roofline["frac_executed"],
+            "kernel_family": {0: "large-K", 1: "small-K two-pass", 2: "SK_U", 3: "SK_Y"}[plan["small_k"]],
             "iteration": {"us": iter_s * 1e6},
             # the kernels the iteration launches (EMEngine.kernels(): the fused small-K E-step
             # has no pass B, the large-K iteration runs pass A, the gene kernel and the update)

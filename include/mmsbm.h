@@ -78,6 +78,29 @@ int mmsbm_set_shape(mmsbm_ctx *ctx, int32_t K, int32_t R, int32_t B, int32_t P, 
 int mmsbm_set_links(mmsbm_ctx *ctx, int32_t which, const int32_t *ids_host,
                     const int32_t *counts_host, int64_t E);
 
+/* Kernel family of the small-K plans (K <= 12; one family above): the three-stream fused
+ * E-step (SK_U) or the stream-0 E-step with Y entries (SK_Y).  Both follow the reference's sums
+ * (:996-1028) and agree with it to ~1e-12; their sums are ordered differently, so a sample's bits
+ * depend on the family, and within one family on nothing else (not B, not the sample's slot, not
+ * the rank).  AUTO picks from B at every mmsbm_set_shape (B = 1: SK_U, the one-sample latency
+ * winner; B >= 2: SK_Y, the throughput winner); a driver whose engines hold different B for one
+ * run (a ragged last batch, ranks with unequal shares, a pool that shrinks) fixes the family from
+ * its configured batch instead, so every sample of the run gets the same bits.  A change of the
+ * effective family drops the link plans (call mmsbm_set_links again).  The environment variable
+ * MMSBM_SK_Y=0/1 overrides it (measurement).  Replaces nothing in the reference (a scheduling
+ * choice of this engine). */
+#define MMSBM_FAMILY_AUTO 0
+#define MMSBM_FAMILY_SKU 1
+#define MMSBM_FAMILY_SKY 2
+int mmsbm_set_family(mmsbm_ctx *ctx, int32_t family);
+
+/* Active samples: mmsbm_iterate, mmsbm_loglik, mmsbm_accumulate, mmsbm_mstep and mmsbm_predict
+ * process samples [0, n) of the B and leave the others untouched (n = 0 or n >= B: all B; the
+ * default).  A restart driver that retires converged samples compacts the live ones to the front
+ * and shrinks n instead of iterating finished slots (the reference ends a sample at convergence,
+ * :1270-1276).  mmsbm_set_shape resets it to B. */
+int mmsbm_set_active(mmsbm_ctx *ctx, int32_t n);
+
 /* deg_host[P]: the degree the M-step divides by (:1016-1018) — for a
  * link-sharded rank the counter over ALL train links, not its own block.  A
  * zero makes mmsbm_iterate / mmsbm_mstep fail with MMSBM_ERR_ZERO_DEGREE.

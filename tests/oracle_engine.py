@@ -6,32 +6,68 @@ import numpy as np
 from oracle import c_oracle
 
 
-class OracleEngine:
-    def __init__(self, links, test_links):
+class _Slots:
+    """EMEngine's sample-slot interface (restarts.run_pool) over per-sample host arrays."""
+
+    def _slots(self, B):
+        if getattr(self, "theta", None) is None or len(self.theta) != B:
+            self.theta, self.pr = [None] * B, [None] * B
+        self.B = B
+        self.active = getattr(self, "active", B)
+
+    def upload_slot(self, b, theta, pr):
+        self.theta[b] = np.array(theta, dtype=np.float64)
+        self.pr[b] = np.array(pr, dtype=np.float64)
+
+    def download_slot(self, b):
+        return self.theta[b].copy(), self.pr[b].copy()
+
+    def move_slot(self, dst, src):
+        if dst != src:
+            self.theta[dst], self.pr[dst] = self.theta[src].copy(), self.pr[src].copy()
+
+    def set_active(self, n):
+        assert 0 < n <= self.B
+        self.active = n
+        self.log.append(("active", n))
+
+    def _live(self):
+        return range(min(self.active, len(self.theta)))
+
+
+class OracleEngine(_Slots):
+    def __init__(self, links, test_links, B=None):
         self.ids, self.counts = c_oracle.links_to_arrays(links)
         self.tids, self.tcounts = c_oracle.links_to_arrays(test_links)
+        self.log = []          # ("iterate", n, live slots) / ("active", n): what the driver asked
+        self.theta = None
+        if B is not None:
+            self._slots(B)
 
     def upload(self, theta, pr):
         self.theta = [np.array(t) for t in theta]
         self.pr = [np.array(p) for p in pr]
+        self.B = self.active = len(self.theta)
 
     def iterate(self, n):
+        self.log.append(("iterate", n, self.active))
         for _ in range(n):
-            for s in range(len(self.theta)):
+            for s in self._live():
                 self.theta[s], self.pr[s] = c_oracle.make_iteration(self.ids, self.counts,
                                                                     self.theta[s], self.pr[s])
 
     def loglik(self, which):
         ids, counts = (self.ids, self.counts) if which == 0 else (self.tids, self.tcounts)
-        if ids.shape[0] == 0:
-            return np.zeros(len(self.theta))
-        return np.array([c_oracle.loglik(ids, counts, t, p) for t, p in zip(self.theta, self.pr)])
+        out = np.full(len(self.theta), np.nan)
+        for s in self._live():
+            out[s] = c_oracle.loglik(ids, counts, self.theta[s], self.pr[s]) if ids.shape[0] else 0.0
+        return out
 
     def download(self):
         return np.stack(self.theta), np.stack(self.pr)
 
 
-class OracleShardEngine:
+class OracleShardEngine(_Slots):
     """CPU stand-in for the link-sharded EMEngine methods (set_links with a global degree,
     accumulate, mstep) on oracle/shard_oracle.py, B batched samples."""
 
@@ -40,6 +76,9 @@ class OracleShardEngine:
         self.device = "cpu"
         self.sets = {}
         self.deg = None
+        self.log = []
+        self.theta = None
+        self._slots(B)
 
     def set_links(self, which, ids, counts, deg=None):
         self.sets[which] = (np.asarray(ids, np.int32), np.asarray(counts, np.int32))
@@ -58,22 +97,23 @@ class OracleShardEngine:
         import torch
         from oracle import shard_oracle
         ids, counts = self.sets[0]
-        for b in range(self.B):
+        for b in self._live():
             n, s = shard_oracle.accumulate(ids, counts, self.theta[b], self.pr[b], self.eps)
             nth[b].copy_(torch.from_numpy(n))
             S[b].copy_(torch.from_numpy(s))
 
     def mstep(self, nth, S):
         from oracle import shard_oracle
-        for b in range(self.B):
+        for b in self._live():
             self.theta[b], self.pr[b] = shard_oracle.mstep(self.theta[b], self.pr[b], nth[b].numpy(),
                                                            S[b].numpy(), self.deg, self.eps)
 
     def loglik(self, which):
         ids, counts = self.sets[which]
-        if ids.shape[0] == 0:
-            return np.zeros(self.B)
-        return np.array([c_oracle.loglik(ids, counts, t, p) for t, p in zip(self.theta, self.pr)])
+        out = np.full(self.B, np.nan)
+        for b in self._live():
+            out[b] = c_oracle.loglik(ids, counts, self.theta[b], self.pr[b]) if ids.shape[0] else 0.0
+        return out
 
 
 class OracleJointEngine:

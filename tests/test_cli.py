@@ -133,7 +133,7 @@ def test_batch_mode_matches_reference_loop(tmp_path):
         rc = cli.main(["-k", "2", "-i", "40", "-n", "3", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST,
                        "-o", out, "--seed", "5", "--batch", "2"], model_factory=factory,
                       out=lines.append,
-                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links))
+                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links, B=n))
     assert rc == 0
     ref = _reference_loop(2, 5, 3, 40, 3, 4)
     got = [l for l in lines if l.startswith("Sample ") and "iterations" in l]
@@ -158,11 +158,13 @@ class _FileModel:
         return M()
 
 
-def _ranked_worker(rank, world, port, argv, queue):
+def _ranked_worker(rank, world, port, argv, queue, pid=None):
     import torch.distributed as dist  # noqa: F401
     from oracle_engine import OracleEngine
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
+    if pid is not None:                       # each rank's default seed (:1149) differs
+        os.getpid = lambda: pid + rank
     holder = {}
 
     def factory():
@@ -173,22 +175,76 @@ def _ranked_worker(rank, world, port, argv, queue):
     with contextlib.redirect_stdout(io.StringIO()):
         rc = cli.main(argv + ["--gpus", str(world), "--backend", "gloo"], model_factory=factory,
                       out=lines.append,
-                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links))
+                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links, B=n))
     queue.put((rank, rc, lines))
 
 
+def _pool_run(argv, out_dir, engines=None):
+    """One-process cli.main with the C oracle as the pool's engine; returns (rc, lines)."""
+    from oracle_engine import OracleEngine
+    holder = {}
+
+    def factory():
+        holder["m"] = _FileModel.make()
+        return holder["m"]
+
+    def eng(n):
+        e = OracleEngine(holder["m"].links, holder["m"].test_links, B=n)
+        if engines is not None:
+            engines.append(e)
+        return e
+    lines = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        rc = cli.main(argv + ["-o", str(out_dir) + os.sep], model_factory=factory, out=lines.append,
+                      engine_factory=eng)
+    return rc, lines
+
+
+def test_pool_refills_converged_slots_and_matches_the_sequential_loop(tmp_path):
+    """--batch 4 over 16 samples (restarts.run_pool): a converged sample's slot goes to the next
+    pending sample at once, the slots shrink when nothing is pending, and the files equal a
+    16-slot run's (no refill) byte for byte; iterations and convergence per sample are the
+    sequential reference loop's (:1253-1279)."""
+    base = ["-k", "2", "-i", "60", "-n", "16", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST, "--seed", "8"]
+    a, b = tmp_path / "b4", tmp_path / "b16"
+    a.mkdir()
+    b.mkdir()
+    engines = []
+    rc, lines4 = _pool_run(base + ["--batch", "4"], a, engines)
+    assert rc == 0 and len(engines) == 1 and engines[0].B == 4
+    rc, lines16 = _pool_run(base + ["--batch", "16"], b)
+    assert rc == 0
+    ref = _reference_loop(2, 8, 16, 60, 3, 4)
+    summary = lambda ls: [l for l in ls if l.startswith("Sample ") and "iterations" in l]  # noqa: E731
+    got = [(int(l.split()[1][:-1]), int(l.split()[2])) for l in summary(lines4)]
+    assert got == [(s, it) for s, it, _ in ref]
+    assert summary(lines4) == summary(lines16)
+    files = sorted(os.listdir(a))
+    assert files == sorted("Sample_%d_K2.csv" % s for s, _, c in ref if c) and files
+    assert files == sorted(os.listdir(b))
+    for f in files:
+        assert (a / f).read_bytes() == (b / f).read_bytes()
+    log = engines[0].log
+    # the pool never iterates a finished sample: slot-iterations = the samples' own iterations
+    slot_its = sum(n * live for kind, n, *rest in log if kind == "iterate" for live in rest)
+    assert slot_its == sum(it for _, it, _ in ref)
+    shrinks = [n for kind, n, *rest in log if kind == "active"]
+    assert shrinks[0] == 4 and shrinks[-1] >= 1 and sorted(shrinks, reverse=True) == shrinks
+
+
 def test_two_rank_gloo_cli_writes_the_one_rank_files(tmp_path):
-    """`--gpus 2` (two ranks, gloo, the C oracle as each rank's engine): the Sample_<n>_K<k>.csv
-    files are byte-identical to a one-process `--batch` run's, and rank 0 prints every sample's
-    summary line in sample order (src/run.sh:36-45, :1253-1279)."""
+    """`--gpus 2` (two ranks, gloo, the C oracle as each rank's engine) with a 4-slot pool per
+    rank over 16 samples: the Sample_<n>_K<k>.csv files are byte-identical to a one-process
+    `--batch 4` run's, and rank 0 prints every sample's summary line in sample order (VERDICT r3
+    item 5, r4 item 2; src/run.sh:36-45, :1253-1279)."""
     import multiprocessing as mp
 
     from oracle_engine import OracleEngine
     one, two = tmp_path / "one", tmp_path / "two"
     one.mkdir()
     two.mkdir()
-    base = ["-k", "2", "-i", "40", "-n", "5", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST, "--seed", "5",
-            "--batch", "2"]
+    base = ["-k", "2", "-i", "40", "-n", "16", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST, "--seed", "5",
+            "--batch", "4"]
     holder = {}
 
     def factory():
@@ -198,7 +254,7 @@ def test_two_rank_gloo_cli_writes_the_one_rank_files(tmp_path):
     lines1 = []
     with contextlib.redirect_stdout(io.StringIO()):
         rc = cli.main(base + ["-o", str(one) + os.sep], model_factory=factory, out=lines1.append,
-                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links))
+                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links, B=n))
     assert rc == 0
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -226,3 +282,54 @@ def test_gpus_flag_validation():
     assert rc == 2
     rc, _ = _run(["--gpus", "2", "--backend", "mpi"])
     assert rc == 2
+
+
+def test_two_ranks_without_seed_replay_rank0_stream(tmp_path):
+    """ADVICE r4: under an external launcher a rank given no --seed seeds from its own pid (:1149);
+    the ranks take rank 0's seed, so the files equal a one-process run seeded with it."""
+    import multiprocessing as mp
+    one, two = tmp_path / "one", tmp_path / "two"
+    one.mkdir()
+    two.mkdir()
+    base = ["-k", "2", "-i", "40", "-n", "6", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST, "--batch", "2"]
+    rc, lines1 = _pool_run(base + ["--seed", "4100"], one)
+    assert rc == 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 410) % 1000
+    procs = [ctx.Process(target=_ranked_worker, args=(r, 2, port, base + ["-o", str(two) + os.sep], q, 4100))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {r: (rc, lines) for r, rc, lines in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert got[0][0] == 0 and got[1][0] == 0
+    files = sorted(os.listdir(one))
+    assert files and files == sorted(os.listdir(two))
+    for f in files:
+        assert (one / f).read_bytes() == (two / f).read_bytes()
+
+
+def test_first_failing_rank_ends_the_launch():
+    """the self-spawn launcher watches every rank; when rank 1 exits 1 while rank 0
+    would wait (in a barrier, here a sleep), rank 0 is terminated and the launch returns 1 at
+    once instead of after rank 0's timeout."""
+    import sys
+    import time
+
+    from trigenicinteractionpredictor_amd.launch import spawn_ranks
+    t0 = time.time()
+    rc = spawn_ranks([sys.executable, "-c", "import os, sys, time\n"
+                      "sys.exit(1) if os.environ['RANK'] == '1' else time.sleep(120)"], 2)
+    assert rc == 1 and time.time() - t0 < 30
+
+
+def test_nccl_ranks_beyond_visible_gpus_are_refused(monkeypatch):
+    """with the nccl backend --gpus above the visible GPUs is exit code 2 (RCCL takes
+    one GPU per rank); gloo may share."""
+    from trigenicinteractionpredictor_amd import launch
+    monkeypatch.setattr(launch, "visible_gpus", lambda: 1)
+    rc, lines = _run(["--gpus", "2", "-t", TRAIN, "-e", TEST, "-k", "2"])
+    assert rc == 2 and any("visible" in l for l in lines)

@@ -86,3 +86,75 @@ def test_cli_gpus_2_on_one_gpu_writes_the_batch_files(tmp_path):
         assert (one / f).read_bytes() == (two / f).read_bytes(), f
     summary = [l for l in p.stdout.splitlines() if l.startswith("Sample ") and "iterations" in l]
     assert [int(l.split()[1][:-1]) for l in summary] == [0, 1, 2, 3]
+
+
+@pytest.mark.parametrize("K,env", [(3, {"MMSBM_SK_Y": "1"})])
+def test_cli_pool_writes_the_sequential_files(tmp_path, monkeypatch, K, env):
+    """`--batch 8` over 16 samples (restarts.run_pool: converged slots refilled at once, the pool
+    shrinking at the end) writes the Sample files of the sequential run (the drop-in Model, one
+    sample at a time, :1253-1279) byte for byte.  One kernel family for both runs: SK_Y forced
+    (the pool's family; the one-sample Model would take SK_U)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    seq, pool = tmp_path / "seq", tmp_path / "pool"
+    seq.mkdir()
+    pool.mkdir()
+    base = ["-k", str(K), "-i", "80", "-n", "16", "-f", "4", "-b", "6", "-t", TRAIN, "-e", TEST, "--seed", "11"]
+    lines = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        assert cli.main(base + ["-o", str(seq) + os.sep], out=lines.append) == 0
+        stats = {}
+        orig = cli._pool
+
+        def spy(*a, **k):
+            from trigenicinteractionpredictor_amd.restarts import PoolStats
+            st = PoolStats()
+            res = orig(*a[:5], a[5], st)
+            stats["s"] = st
+            return res
+        monkeypatch.setattr(cli, "_pool", spy)
+        assert cli.main(base + ["-o", str(pool) + os.sep, "--batch", "8"], out=lambda *_: None) == 0
+    files = sorted(os.listdir(seq))
+    assert files and files == sorted(os.listdir(pool))
+    for f in files:
+        assert (seq / f).read_bytes() == (pool / f).read_bytes(), f
+    st = stats["s"]
+    assert st.refills >= 1 and st.slot_iterations == st.sample_iterations
+
+
+@pytest.mark.parametrize("K,family", [(10, "sky"), (13, "auto")])
+def test_pool_results_equal_single_sample_runs(tmp_path, K, family):
+    """restarts.run_pool with 4 slots over 10 samples (refills, then shrinking): every sample's
+    final theta / p / likelihood equals, bit for bit, a one-sample engine of the same family run
+    for the same number of iterations, converged or not (the large-K case rarely converges on
+    small data, so this compares parameters rather than files)."""
+    import random
+    from trigenicinteractionpredictor_amd import EMEngine, Model
+    from trigenicinteractionpredictor_amd.data import FoldSpec, write_fold
+    from trigenicinteractionpredictor_amd.restarts import PoolStats, run_pool, stream_states
+    tr, te = str(tmp_path / "tr.dat"), str(tmp_path / "te.dat")
+    write_fold(FoldSpec(P=120, E=1500, seed=K), tr, te)
+    m = Model()
+    m.get_traintest(tr, te)
+
+    def engine(B):
+        e = EMEngine(K, m.P, B=B, family=family)
+        e.set_links(0, *m._link_arrays(0))
+        e.set_links(1, *m._link_arrays(1))
+        return e
+    random.seed(3)
+    st = PoolStats()
+    res = run_pool(engine(4), stream_states(m, K, range(10)), iterations=40, fcheck=3, bcheck=5,
+                   keep_params=True, stats=st)
+    assert sorted(r.sample for r in res) == list(range(10)) and st.refills == 6
+    assert st.slot_iterations == sum(r.iterations for r in res)
+    random.seed(3)
+    init = {s: (th, pr) for s, th, pr in stream_states(m, K, range(10))}
+    for r in res:
+        one = engine(1)
+        one.upload(init[r.sample][0][None], init[r.sample][1][None])
+        one.iterate(r.iterations)
+        th, pr = one.download()
+        np.testing.assert_array_equal(th[0], r.theta)
+        np.testing.assert_array_equal(pr[0], r.pr)
+        assert one.loglik(0)[0] == r.loglik

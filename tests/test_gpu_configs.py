@@ -317,7 +317,7 @@ def test_restart_driver_on_gpu_matches_oracle_driver(tmp_path):
     th, pr = init_samples(m, 4, ids, seed=8)
     eng = _engine(m, 4, 4, th, pr)
     got = run_samples(eng, ids, th, pr, iterations=60, fcheck=5, bcheck=10)
-    want = run_samples(OracleEngine(m.links, m.test_links), ids, th, pr, iterations=60, fcheck=5,
+    want = run_samples(OracleEngine(m.links, m.test_links, B=len(ids)), ids, th, pr, iterations=60, fcheck=5,
                        bcheck=10)
     for g, w in zip(got, want):
         assert (g.sample, g.iterations, g.converged) == (w.sample, w.iterations, w.converged)

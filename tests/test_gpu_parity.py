@@ -238,37 +238,123 @@ def test_batched_engine_matches_oracle(tmp_path, K, P, E, B):
         np.testing.assert_allclose(L[b], c_oracle.loglik(ids, counts, th_o, pr_o), rtol=RTOL)
 
 
-def test_batched_samples_match_single_runs_bitwise(tmp_path):
-    """A sample's bits do not depend on its batch-mates or the batch size: the work plan is
-    the same for every B (so restart sharding over 1 or 8 GPUs gives identical samples)."""
+@pytest.mark.parametrize("K", [4, 10, 13])
+def test_batched_samples_match_single_runs_bitwise(tmp_path, K):
+    """Within one kernel family a sample's bits do not depend on its batch-mates, the batch size
+    or its slot (the work plan is the same for every B), so restart sharding over 1 or 8 GPUs and
+    the restart pool give identical samples (include/mmsbm.h mmsbm_set_family).
+    Both small-K families (SK_U, SK_Y; K > 12 has one) are run at B = 3 and B = 1 and compared
+    bit for bit, and each agrees with the C oracle at the parity tolerance."""
+    from oracle import c_oracle
     from trigenicinteractionpredictor_amd import EMEngine, Model
     from trigenicinteractionpredictor_amd.layout import links_to_arrays
     tr, te = _fold(tmp_path, 200, 2000, seed=3)
     m = Model()
     m.get_traintest(tr, te)
-    K, B = 4, 3
+    B = 3
     random.seed(77)
     thetas, prs = [], []
     for _ in range(B):
         m.initialize_parameters(K)
         thetas.append(np.array(m.theta))
         prs.append(np.array(m.pr))
-    eng = EMEngine(K, m.P, B=B)
-    eng.set_links(0, *links_to_arrays(m.links))
-    eng.set_links(1, *links_to_arrays(m.test_links))
-    eng.upload(np.stack(thetas), np.stack(prs))
-    eng.iterate(4)
-    th_b, pr_b = eng.download()
-    L_b = eng.loglik(0)
+    ids, counts = links_to_arrays(m.links)
+    tids, tcounts = links_to_arrays(m.test_links)
+    oracle = []
     for s in range(B):
-        single = Model()
-        single.get_traintest(tr, te)
-        single.K = K
-        single.theta, single.pr = thetas[s].tolist(), prs[s].tolist()
-        single.make_iterations(4)
-        np.testing.assert_array_equal(np.array(single.theta), th_b[s])
-        np.testing.assert_array_equal(np.array(single.pr), pr_b[s])
-        assert single.compute_likelihood() == L_b[s]
+        th_o, pr_o = thetas[s], prs[s]
+        for _ in range(4):
+            th_o, pr_o = c_oracle.make_iteration(ids, counts, th_o, pr_o)
+        oracle.append((th_o, pr_o))
+    for family in (("sku", "sky") if K <= 12 else ("auto",)):
+        eng = EMEngine(K, m.P, B=B, family=family)
+        eng.set_links(0, ids, counts)
+        eng.set_links(1, tids, tcounts)
+        assert eng.plan_info()["small_k"] == {"sku": 2, "sky": 3, "auto": 0}[family]
+        eng.upload(np.stack(thetas), np.stack(prs))
+        eng.iterate(4)
+        th_b, pr_b = eng.download()
+        L_b = eng.loglik(0)
+        for s in range(B):
+            one = EMEngine(K, m.P, B=1, family=family)
+            one.set_links(0, ids, counts)
+            one.upload(thetas[s][None], prs[s][None])
+            one.iterate(4)
+            th1, pr1 = one.download()
+            np.testing.assert_array_equal(th1[0], th_b[s])
+            np.testing.assert_array_equal(pr1[0], pr_b[s])
+            assert one.loglik(0)[0] == L_b[s]
+            np.testing.assert_allclose(th_b[s], oracle[s][0], rtol=RTOL, atol=ATOL)
+            np.testing.assert_allclose(pr_b[s], oracle[s][1], rtol=RTOL, atol=ATOL)
+
+
+def test_family_defaults_follow_batch_size(tmp_path):
+    """MMSBM_FAMILY_AUTO: SK_U for one sample (the drop-in Model), SK_Y from two."""
+    from trigenicinteractionpredictor_amd import EMEngine, Model
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    tr, te = _fold(tmp_path, 100, 800, seed=4)
+    m = Model()
+    m.get_traintest(tr, te)
+    random.seed(1)
+    m.initialize_parameters(6)
+    m.make_iteration()
+    assert m._engine.plan_info()["small_k"] == 2
+    for B, want in ((1, 2), (2, 3), (5, 3)):
+        eng = EMEngine(6, m.P, B=B)
+        eng.set_links(0, *links_to_arrays(m.links))
+        assert eng.plan_info()["small_k"] == want
+
+
+@pytest.mark.parametrize("K", [10, 20])
+def test_active_prefix_and_slot_moves_keep_bits(tmp_path, K):
+    """mmsbm_set_active / EMEngine.move_slot / upload_slot (the restart pool's operations): slots
+    outside the active prefix are not touched, and a sample moved between slots mid-run ends
+    bitwise equal to an uninterrupted single run of the same family."""
+    from trigenicinteractionpredictor_amd import EMEngine, Model
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    tr, te = _fold(tmp_path, 150, 1500, seed=5)
+    m = Model()
+    m.get_traintest(tr, te)
+    random.seed(2)
+    th, pr = [], []
+    for _ in range(4):
+        m.initialize_parameters(K)
+        th.append(np.array(m.theta))
+        pr.append(np.array(m.pr))
+    ids, counts = links_to_arrays(m.links)
+    eng = EMEngine(K, m.P, B=4, family="sky")
+    eng.set_links(0, ids, counts)
+    for b in range(4):
+        eng.upload_slot(b, th[b], pr[b])
+    eng.iterate(2)
+    eng.set_active(2)                      # slots 2, 3 frozen
+    frozen = eng.download()
+    eng.iterate(3)
+    L = eng.loglik(0)
+    assert np.isnan(L[2:]).all() and np.isfinite(L[:2]).all()
+    now = eng.download()
+    np.testing.assert_array_equal(now[0][2:], frozen[0][2:])
+    np.testing.assert_array_equal(now[1][2:], frozen[1][2:])
+    eng.move_slot(0, 1)                    # sample 1 continues in slot 0
+    eng.upload_slot(1, th[3], pr[3])       # slot 1: sample 3 from its initial state
+    eng.iterate(1)
+    th_b, pr_b = eng.download()
+
+    def single(s, n):
+        one = EMEngine(K, m.P, B=1, family="sky")
+        one.set_links(0, ids, counts)
+        one.upload(th[s][None], pr[s][None])
+        one.iterate(n)
+        return one.download()
+    t1, p1 = single(1, 6)
+    np.testing.assert_array_equal(th_b[0], t1[0])
+    np.testing.assert_array_equal(pr_b[0], p1[0])
+    t3, p3 = single(3, 1)
+    np.testing.assert_array_equal(th_b[1], t3[0])
+    np.testing.assert_array_equal(pr_b[1], p3[0])
+    td, pd = eng.download_slot(1)
+    np.testing.assert_array_equal(td, t3[0])
+    np.testing.assert_array_equal(pd, p3[0])
 
 
 def test_bitwise_reproducible(tmp_path):

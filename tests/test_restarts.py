@@ -77,7 +77,7 @@ def test_batched_driver_matches_reference_loop():
     ref = _reference_driver(K, seed, n, iters, f, b)
     m = _host()
     th, pr = init_samples(m, K, list(range(n)), seed)
-    res = run_samples(OracleEngine(m.links, m.test_links), list(range(n)), th, pr, iters, f, b)
+    res = run_samples(OracleEngine(m.links, m.test_links, B=n), list(range(n)), th, pr, iters, f, b)
     for r, (s, it, conv, like) in zip(res, ref):
         assert (r.sample, r.iterations, r.converged) == (s, it, conv)
         assert r.loglik == like
@@ -89,7 +89,7 @@ def _worker(rank, world, port, queue):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m = _host()
     res = run_restarts(m, 2, 5, seed=5, iterations=30, fcheck=3, bcheck=4,
-                       engine_factory=lambda B: OracleEngine(m.links, m.test_links))
+                       engine_factory=lambda B: OracleEngine(m.links, m.test_links, B=B))
     queue.put((rank, [(r.sample, r.iterations, r.converged, r.loglik, r.heldout) for r in res]))
     dist.barrier()
     dist.destroy_process_group()
@@ -108,7 +108,7 @@ def test_two_rank_gloo_gather_matches_single_process():
         assert p.exitcode == 0
     m = _host()
     single = run_restarts(m, 2, 5, seed=5, iterations=30, fcheck=3, bcheck=4,
-                          engine_factory=lambda B: OracleEngine(m.links, m.test_links))
+                          engine_factory=lambda B: OracleEngine(m.links, m.test_links, B=B))
     want = [(r.sample, r.iterations, r.converged, r.loglik, r.heldout) for r in single]
     assert got[0] == want and got[1] == want
 

@@ -139,3 +139,27 @@ def test_joint_model_deepcopy_and_alias():
     clone = copy.deepcopy(mj)
     assert isinstance(clone.links, TrackedLinks) and clone.links == mj.links
     assert version_of(clone.links) and version_of(clone.dlinks)
+
+
+def test_one_dict_backing_two_tables_reaches_both():
+    """ADVICE r4: a dict assigned to two tables (two Models here) keeps one row object per key;
+    the rows notify both tables, so `d[k][r] += 1` and an edit through a row reference taken
+    before the second assignment reach both devices' keys; a key added through one table reaches
+    `d` and the other table at its links_changed()."""
+    d = {"0_1_2": [1, 0], "1_2_3": [0, 1]}
+    a, b = Model(), Model()
+    a.links = d
+    row = d["0_1_2"]
+    b.links = d
+    assert d["0_1_2"] is row and a.links["0_1_2"] is row and b.links["0_1_2"] is row
+    va, vb = version_of(a.links), version_of(b.links)
+    d["0_1_2"][1] += 1
+    assert version_of(a.links) != va and version_of(b.links) != vb
+    va, vb = version_of(a.links), version_of(b.links)
+    row[0] = 7
+    assert version_of(a.links) != va and version_of(b.links) != vb
+    assert a.links["0_1_2"] == b.links["0_1_2"] == [7, 1]
+    b.links["5_6_7"] = [1, 1]
+    assert "5_6_7" in d and "5_6_7" not in a.links
+    a.links_changed()
+    assert a.links["5_6_7"] == [1, 1] and a.links["5_6_7"] is b.links["5_6_7"]

@@ -1,4 +1,4 @@
-"""profiles/pmc_<round>_K<K>.json from a tools/gpu_r03_prof.sh output directory: HBM bytes per
+"""profiles/pmc_<round>_K<K>.json from a `tools/gpu.sh TAG prof` output directory: HBM bytes per
 launch of each kernel of the iteration = 2 x FETCH_SIZE (gfx950: FETCH_SIZE tallies 128-B requests
 at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE, both in KiB per dispatch, averaged over the dispatches
 of the PMC passes.  The record is stamped with the build id of the library the passes ran (the

@@ -22,6 +22,9 @@ MMSBM_ERR_ZERO_DEGREE = -3
 MMSBM_ERR_UNSUPPORTED = -4
 SET_TRAIN = 0
 SET_TEST = 1
+FAMILY_AUTO = 0     # mmsbm_set_family: the small-K kernel family from B
+FAMILY_SKU = 1      # the three-stream fused E-step
+FAMILY_SKY = 2      # the stream-0 E-step with Y entries
 CHUNK = 4
 MAX_K = 32
 
@@ -46,6 +49,8 @@ SIGNATURES = {
     "mmsbm_mstep": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "mmsbm_plan_info": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i64)]),
     "mmsbm_set_theta_addend": (_c_int, [_vp, _vp]),
+    "mmsbm_set_family": (_c_int, [_vp, _c_i32]),
+    "mmsbm_set_active": (_c_int, [_vp, _c_i32]),
     "mmsbm_timing": (_c_int, [_vp, _c_i32]),
     "mmsbm_timing_result": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_i64)]),
     "mmsbm_time_kernel": (_c_int, [_vp, _c_i32, _vp, _vp, _c_i32, _vp, ctypes.POINTER(_c_dbl)]),

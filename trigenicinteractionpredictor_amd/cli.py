@@ -199,78 +199,67 @@ def _summary(r):
             + str(r.loglik) + (" (converged)" if r.converged else ""))
 
 
-def _default_engine_factory(model, K):
+def _default_engine_factory(model, K, family):
     from .engine import EMEngine
 
     def factory(n):
-        eng = EMEngine(K, model.P, B=n, R=model.R, eps=model.eps)
+        eng = EMEngine(K, model.P, B=n, R=model.R, eps=model.eps, family=family)
         eng.set_links(0, *model._link_arrays(0))
         eng.set_links(1, *model._link_arrays(1))
         return eng
     return factory
 
 
-def run_batch(model, cfg, samples, out=print, engine_factory=None):
-    """`--batch B`: the pending samples advance B at a time in one batched engine
-    (restarts.run_samples: the reference's per-sample check schedule and convergence rule,
-    :1262-1279, applied to every sample of the batch).  Initial states come from the one RNG
-    stream in sample order, exactly as the sequential loop draws them (:1260); a converged
-    sample's theta / p snapshot is written through `Model.to_file` (:1275) with its converged
-    train likelihood as `likelihood` (:1269).  Returns [(sample, iterations, converged)]."""
-    import numpy as np
-    from .restarts import run_samples
-    K, B = cfg["k"], cfg["batch"]
+def _pool(model, cfg, samples, mine, engine_factory, on_done, stats=None):
+    """One engine of min(--batch, len(mine)) slots over the samples in `mine` (restarts.run_pool):
+    a converged sample's file is written at once (:1275) and its slot goes to the next pending
+    sample.  The kernel family follows the configured --batch (restarts.family_for_batch), so
+    every sample's bits are those of the one-process run whatever its share."""
+    from .restarts import family_for_batch, run_pool, stream_states
+    K = cfg["k"]
+    n = min(cfg["batch"], len(mine))
+    if n == 0:
+        return []
     if engine_factory is None:
-        engine_factory = _default_engine_factory(model, K)
-    done = []
-    for lo in range(0, len(samples), B):
-        block = samples[lo:lo + B]
-        thetas, prs = [], []
-        for s in block:                        # draws in sample order, like :1260
-            model.initialize_parameters(K)
-            thetas.append(np.array(model._theta, dtype=np.float64))
-            prs.append(np.array(model._pr, dtype=np.float64))
-        res = run_samples(engine_factory(len(block)), block, thetas, prs, cfg["iterations"],
-                          cfg["fcheck"], cfg["bcheck"], keep_params=True)
-        for r in res:
-            out(_summary(r))
-            if r.converged:
-                _write_result(model, cfg, r)
-            done.append((r.sample, r.iterations, r.converged))
-    return done
+        engine_factory = _default_engine_factory(model, K, family_for_batch(cfg["batch"]))
+    return run_pool(engine_factory(n), stream_states(model, K, samples, mine), cfg["iterations"],
+                    cfg["fcheck"], cfg["bcheck"], keep_params=True, on_done=on_done, stats=stats)
 
 
-def run_ranked(model, cfg, samples, out=print, engine_factory=None, group=None, device=None):
+def run_batch(model, cfg, samples, out=print, engine_factory=None, stats=None):
+    """`--batch B`: the pending samples share one B-slot engine (restarts.run_pool): the
+    reference's per-sample check schedule and convergence rule (:1262-1279) for each sample; a
+    converged sample is written through `Model.to_file` (:1275) as soon as it converges, with its
+    converged train likelihood as `likelihood` (:1269), and its slot takes the next pending sample
+    at once.  Initial states come from the one RNG stream in sample order (:1260).  The summary
+    lines print in sample order at the end.  Returns [(sample, iterations, converged)]."""
+    def done(r):
+        if r.converged:
+            _write_result(model, cfg, r)
+    res = sorted(_pool(model, cfg, samples, set(samples), engine_factory, done, stats),
+                 key=lambda r: r.sample)
+    for r in res:
+        out(_summary(r))
+    return [(r.sample, r.iterations, r.converged) for r in res]
+
+
+def run_ranked(model, cfg, samples, out=print, engine_factory=None, group=None, device=None, stats=None):
     """`--gpus N`, one rank: this rank's contiguous block of the pending `samples` (the same list
-    on every rank), advanced `--batch` at a time with the reference's per-sample check schedule
-    and convergence rule (restarts.run_samples), converged samples written by this rank; then
-    one all-gather (restarts.gather_results: RCCL over xGMI under nccl) of every rank's
-    (sample, iterations, converged, likelihood, held-out likelihood).  Rank 0 prints one summary
-    line per sample, in sample order, as run_batch does.  Returns the gathered results."""
-    import numpy as np
+    on every rank) in one `--batch`-slot pool (restarts.run_pool: the reference's per-sample check
+    schedule and convergence rule, converged samples written by this rank at once, freed slots
+    refilled from the block); then one all-gather (restarts.gather_results: RCCL over xGMI under
+    nccl) of every rank's (sample, iterations, converged, likelihood, held-out likelihood).  Rank 0
+    prints one summary line per sample, in sample order, as run_batch does.  Returns the gathered
+    results."""
     import torch.distributed as dist
-    from .restarts import gather_results, run_samples, shard_samples
+    from .restarts import gather_results, shard_samples
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    K, B = cfg["k"], cfg["batch"]
-    mine = set(shard_samples(len(samples), world, rank))
-    states = {}
-    for i, s in enumerate(samples):          # the one stream, in sample order (:1260)
-        model.initialize_parameters(K)
-        if i in mine:
-            states[s] = (np.array(model._theta, dtype=np.float64), np.array(model._pr, dtype=np.float64))
-    block = [s for i, s in enumerate(samples) if i in mine]
-    if block and engine_factory is None:
-        engine_factory = _default_engine_factory(model, K)
-    local = []
-    for lo in range(0, len(block), B):
-        part = block[lo:lo + B]
-        res = run_samples(engine_factory(len(part)), part, [states[s][0] for s in part],
-                          [states[s][1] for s in part], cfg["iterations"], cfg["fcheck"], cfg["bcheck"],
-                          keep_params=True)
-        for r in res:
-            if r.converged:
-                _write_result(model, cfg, r)
-        local += res
+    mine = {samples[i] for i in shard_samples(len(samples), world, rank)}
+
+    def done(r):
+        if r.converged:
+            _write_result(model, cfg, r)
+    local = _pool(model, cfg, samples, mine, engine_factory, done, stats)
     rows = gather_results(local, len(samples), group=group, device=device)
     if rank == 0:
         for r in rows:
@@ -280,30 +269,28 @@ def run_ranked(model, cfg, samples, out=print, engine_factory=None, group=None, 
 
 def spawn_ranks(n, argv):
     """`--gpus N` without a launcher: N copies of this command, one rank per GPU, started before
-    this process touches a GPU; returns the worst exit code.  The parent's seed is passed on, so
-    every rank replays the same RNG stream (:1149 seeds it once per run)."""
-    import socket
-    import subprocess
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
+    this process touches a GPU; every rank is watched at once and the first failure ends the
+    others (launch.wait_ranks).  The parent's seed is passed on, so every rank replays the same
+    RNG stream (:1149 seeds it once per run)."""
+    from .launch import spawn_ranks as spawn
     if not any(a == "--seed" or a.startswith("--seed=") for a in argv):
         argv = list(argv) + ["--seed", str(os.getpid())]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, "-m", "trigenicinteractionpredictor_amd.cli", *argv],
-                                      env=env))
-    rc = 0
-    for p in procs:
-        code = p.wait()
-        if code != 0:
-            rc = rc or (code if code > 0 else 128 - code)
-            for q in procs:
-                if q.poll() is None:
-                    q.terminate()
-    return rc
+    return spawn([sys.executable, "-m", "trigenicinteractionpredictor_amd.cli", *argv], n)
+
+
+def _too_many_ranks(cfg, out):
+    """RCCL takes one GPU per rank: --gpus above the visible GPUs would put two ranks of one
+    communicator on one device (refused or hung), so it is an argument error (gloo ranks may
+    share a GPU: a rehearsal mode)."""
+    if cfg["backend"] != "nccl":
+        return False
+    from .launch import visible_gpus
+    n = visible_gpus()
+    if cfg["gpus"] > n:
+        out("\n\nERROR: --gpus %d with the nccl backend needs %d GPUs, %d visible (--backend gloo "
+            "shares GPUs)" % (cfg["gpus"], cfg["gpus"], n))
+        return True
+    return False
 
 
 def main(argv=None, model_factory=None, out=print, engine_factory=None):
@@ -317,6 +304,8 @@ def main(argv=None, model_factory=None, out=print, engine_factory=None):
     if cfg.get("help"):
         return 0
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if cfg["gpus"] > 1 and _too_many_ranks(cfg, out):
+        return 2
     if cfg["gpus"] > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(cfg["gpus"], argv)                   # before any GPU call
     if world != cfg["gpus"]:
@@ -337,6 +326,11 @@ def main(argv=None, model_factory=None, out=print, engine_factory=None):
             if torch.cuda.is_available():           # ranks sharing the box's GPUs (rehearsal)
                 torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
             dist.init_process_group("gloo")
+        # one RNG stream for the run (:1149): under an external launcher a rank given no --seed
+        # seeded from its own pid, so every rank takes rank 0's seed
+        box = [cfg["seed"]]
+        dist.broadcast_object_list(box, src=0)
+        cfg["seed"] = box[0]
         if rank != 0:
             out = _quiet
     try:

@@ -1347,7 +1347,9 @@ struct mmsbm_ctx {
   int gcap = 0;                  // most pivot genes per stream-0 workgroup (<= KT<K>::GMAX)
   bool sk = false;               // K <= 12: the small-K kernels of sk.h (MMSBM_SK=0: the large-K ones)
   bool sk_fused = false;         // small-K: one fused E-step launch (SK_U) instead of pass A + pass B
-  bool sk_y = false;             // small-K fused: the stream-0 E-step with Y entries (SK_Y, MMSBM_SK_Y=1)
+  bool sk_y = false;             // small-K fused: the stream-0 E-step with Y entries (SK_Y)
+  int family = MMSBM_FAMILY_AUTO;  // mmsbm_set_family: SK_U / SK_Y, or from B (AUTO)
+  int nact = 0;                  // mmsbm_set_active: samples [0, nact) run (0: all B)
   SetDev sets[2];
   int* deg = nullptr;            // device, owned
   std::vector<int> deg_host;
@@ -1392,6 +1394,9 @@ struct mmsbm_ctx {
 };
 
 namespace {
+
+// samples the launches cover (grid.y): the active prefix of the B (mmsbm_set_active)
+inline int nb_of(const mmsbm_ctx* c) { return c->nact > 0 && c->nact < c->B ? c->nact : c->B; }
 
 struct WsLayout {
   size_t cbuf, prows, spart, gx, partL, nth, S, total;
@@ -1491,22 +1496,22 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
       HIP_TRY(hipEventRecord(c->ev_fork, s));
       HIP_TRY(hipStreamWaitEvent(c->ys, c->ev_fork, 0));
       const long long nyb = ((long long)c->P * K + 255) / 256;
-      ysum_kernel<K><<<dim3((unsigned)nyb, c->B), 256, 0, c->ys>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
+      ysum_kernel<K><<<dim3((unsigned)nyb, nb_of(c)), 256, 0, c->ys>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
       HIP_TRY(hipGetLastError());
     }
     // two launches from K = 24 (K=30 gene 1,778 -> 1,745 us, profiles/r04w_gsplit_ab.txt); at
     // K = 20-23 two gene workgroups share a CU and the single launch, whose S and Y workgroups
     // overlap the x0 ones, is faster (K=20 x 8: 129.5 vs 154.7 us, profiles/r04v_gsplit_ab.txt)
     if (c->gsplit && K >= 24) {  // x0 workgroups, then the S and Y workgroups at their own budget
-      gene_kernel<K><<<dim3(ngw, c->B), F::NT, F::LDS, s>>>(
+      gene_kernel<K><<<dim3(ngw, nb_of(c)), F::NT, F::LDS, s>>>(
           theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
           c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, 0);
       HIP_TRY(hipGetLastError());
-      gene_sy_kernel<K><<<dim3(nspw + nyw, c->B), F::NT, F::LDS_SP * 8, s>>>(
+      gene_sy_kernel<K><<<dim3(nspw + nyw, nb_of(c)), F::NT, F::LDS_SP * 8, s>>>(
           theta, c->prows, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx + pk, c->spart, c->P, h.n_prows,
           h.n_y, std::max(h.n_sp, 1), nspw);
     } else {
-      gene_kernel<K><<<dim3(ngw + nspw + nyw, c->B), F::NT, F::LDS, s>>>(
+      gene_kernel<K><<<dim3(ngw + nspw + nyw, nb_of(c)), F::NT, F::LDS, s>>>(
           theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
           c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, nspw);
     }
@@ -1521,13 +1526,13 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
     const int lds = (c->gcap * T::VDBL + T::tg_dbl(c->gcap)) * 8 + T::IMG_BYTES + 64;
     if (mode == PASS_A) {
       if ((rc = lds_opt_in(c, 0, &pass_kernel<K, PASS_A>, T::LDS_A))) return rc;
-      pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
+      pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, nb_of(c)), NT, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.row_y, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
           theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, h.n_y, h.n_prows, h.n_wg_a, c->eps, c->gcap,
           h.merge ? 1 : 0);
     } else {
       if ((rc = lds_opt_in(c, 1, &pass_kernel<K, PASS_LL>, T::LDS_A))) return rc;
-      pass_kernel<K, PASS_LL><<<dim3(h.n_wg_a, c->B), NT, lds, s>>>(
+      pass_kernel<K, PASS_LL><<<dim3(h.n_wg_a, nb_of(c)), NT, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, nullptr, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
           theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, 0, h.n_prows, h.n_wg_a, c->eps, c->gcap, 0);
     }
@@ -1554,11 +1559,11 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   // joint model: the q cells (qr M-step from the pair launch's S2 partials), theta update only
   const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
   if (sums)
-    upd_kernel<K, true><<<dim3(nthw + ncw, c->B), UPD_NT, 0, s>>>(
+    upd_kernel<K, true><<<dim3(nthw + ncw, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
         nth, S, c->nth_add, nullptr, nullptr, 0);
   else
-    upd_kernel<K, false><<<dim3(nthw + ncw + nqc, c->B), UPD_NT, 0, s>>>(
+    upd_kernel<K, false><<<dim3(nthw + ncw + nqc, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
         nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg);
   HIP_TRY(hipGetLastError());
@@ -1569,7 +1574,7 @@ template <int K>
 int launch_mapply(mmsbm_ctx* c, double* theta, double* pr, const double* nth, const double* S,
                   hipStream_t s) {
   const long long n = (long long)c->P * K + (long long)K * K * K;
-  mapply_kernel<K><<<dim3((unsigned)((n + 255) / 256), c->B), 256, 0, s>>>(theta, pr, nth, S, c->deg,
+  mapply_kernel<K><<<dim3((unsigned)((n + 255) / 256), nb_of(c)), 256, 0, s>>>(theta, pr, nth, S, c->deg,
                                                                            c->P, c->R, c->eps);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
@@ -1580,7 +1585,7 @@ int launch_predict(mmsbm_ctx* c, const int* ids, long long n, const double* thet
                    const double* pr, double* out, hipStream_t s) {
   if (n == 0) return MMSBM_OK;
   const long long nb = (n + 255) / 256;
-  predict_kernel<K><<<dim3((unsigned)nb, c->B), 256, 0, s>>>(ids, n, theta, pr, out, c->P, c->R);
+  predict_kernel<K><<<dim3((unsigned)nb, nb_of(c)), 256, 0, s>>>(ids, n, theta, pr, out, c->P, c->R);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -1600,31 +1605,31 @@ int launch_sk_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const
   if (mode == PASS_B) {
     if (h.n_wg_b == 0 || c->sk_fused) return MMSBM_OK;  // fused: streams 1, 2 ran in "pass A"
     if ((rc = lds_opt_in(c, 5, &sk_pass_kernel<K, SK_B>, T::LDS_B))) return rc;
-    sk_pass_kernel<K, SK_B><<<dim3(h.n_wg_b, c->B), NT, T::LDS_B, s>>>(
+    sk_pass_kernel<K, SK_B><<<dim3(h.n_wg_b, nb_of(c)), NT, T::LDS_B, s>>>(
         sd.skr[1], sd.sku[1], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, h.n_wg_a,
         h.sk_L[1], c->P, c->R, n_cb, h.n_prows, h.n_wg_b, c->eps, nullptr, nullptr, 0);
   } else if (mode == PASS_A && c->sk_y) {  // SK_Y: the stream-0 E-step with Y entries
     if (h.n_wg_a == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 9, &sky_pass_kernel<K>, SKY<K>::LDS))) return rc;
-    sky_pass_kernel<K><<<dim3(h.n_wg_a, c->B), NT, SKY<K>::LDS, s>>>(
+    sky_pass_kernel<K><<<dim3(h.n_wg_a, nb_of(c)), NT, SKY<K>::LDS, s>>>(
         sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, sec, h.sk_L[0], c->P, c->R,
         h.n_y, h.n_prows, h.n_wg_a, c->eps);
   } else if (mode == PASS_A && c->sk_fused) {  // the fused E-step: every stream in one launch
     if (h.n_wg_a + h.n_wg_b == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 7, &sk_pass_kernel<K, SK_U>, T::LDS_U))) return rc;
-    sk_pass_kernel<K, SK_U><<<dim3(h.n_wg_a + h.n_wg_b, c->B), NT, T::LDS_U, s>>>(
+    sk_pass_kernel<K, SK_U><<<dim3(h.n_wg_a + h.n_wg_b, nb_of(c)), NT, T::LDS_U, s>>>(
         sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
         h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps, sd.skr[1], sd.sku[1], h.sk_L[1]);
   } else if (mode == PASS_A) {
     if (h.n_wg_a == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 4, &sk_pass_kernel<K, SK_A>, T::LDS))) return rc;
-    sk_pass_kernel<K, SK_A><<<dim3(h.n_wg_a, c->B), NT, T::LDS, s>>>(
+    sk_pass_kernel<K, SK_A><<<dim3(h.n_wg_a, nb_of(c)), NT, T::LDS, s>>>(
         sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
         h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps, nullptr, nullptr, 0);
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
     if ((rc = lds_opt_in(c, 6, &sk_pass_kernel<K, SK_LL>, T::LDS))) return rc;
-    sk_pass_kernel<K, SK_LL><<<dim3(h.n_wg_a, c->B), NT, T::LDS, s>>>(
+    sk_pass_kernel<K, SK_LL><<<dim3(h.n_wg_a, nb_of(c)), NT, T::LDS, s>>>(
         sd.skr[0], sd.sku[0], r12, theta, pr, c->cbuf, c->prows, c->spart, c->partL, sec, 0,
         h.sk_L[0], c->P, c->R, n_cb, h.n_prows, h.n_wg_a, c->eps, nullptr, nullptr, 0);
   }
@@ -1648,11 +1653,11 @@ int launch_sk_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nt
   }
   const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
   if (sums)
-    sk_fin_kernel<K, true><<<dim3(ngw + ncw, c->B), SKF_NT, 0, s>>>(
+    sk_fin_kernel<K, true><<<dim3(ngw + ncw, nb_of(c)), SKF_NT, 0, s>>>(
         theta, pr, c->prows, sd.gptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, nullptr, nullptr, 0, yb, sd.yptr, h.n_y);
   else
-    sk_fin_kernel<K, false><<<dim3(ngw + ncw + nqc, c->B), SKF_NT, 0, s>>>(
+    sk_fin_kernel<K, false><<<dim3(ngw + ncw + nqc, nb_of(c)), SKF_NT, 0, s>>>(
         theta, pr, c->prows, sd.gptr, c->spart, c->deg, spr, c->P, c->R, h.n_prows,
         std::max(h.n_wg_a, 1), ngw, c->eps, nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg, yb, sd.yptr,
         h.n_y);
@@ -1735,6 +1740,25 @@ int set_degree(mmsbm_ctx* c, const std::vector<int>& deg) {
     c->deg = nullptr;
   }
   return upload(&c->deg, deg);
+}
+
+// The small-K kernel family (include/mmsbm.h mmsbm_set_family): the stream-0 E-step with Y entries
+// (SK_Y) or the three-stream fused E-step (SK_U).  Same-box A/B (profiles/r04j_sky_ab.txt): SK_Y
+// does less than half SK_U's work and wins where the grid is throughput-bound (fold0 K=10, 8
+// samples: 78.2k vs 62.1k sample-iter/s) but loses at one sample, where both are bound by one
+// wave's latency chain (25.1 vs 23.2 us per iteration), hence AUTO = SK_Y from B = 2.  The two
+// order their sums differently, so the family is part of a sample's bits: drivers fix it per run.
+void apply_family(mmsbm_ctx* c) {
+  bool sky = c->family == MMSBM_FAMILY_SKY || (c->family == MMSBM_FAMILY_AUTO && c->B >= 2);
+  if (const char* y = getenv("MMSBM_SK_Y")) sky = y[0] == '1';  // measurement override
+  sky = sky && c->sk_fused;
+  if (sky != c->sk_y) {  // the plans hold different streams: set links again
+    DeviceGuard g(c->device);
+    for (auto& sd : c->sets) sd.release();
+    c->ws = nullptr;
+    c->ws_bytes = 0;
+  }
+  c->sk_y = sky;
 }
 
 }  // namespace
@@ -1845,21 +1869,9 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
       c->ws_bytes = 0;
     }
     c->sk_fused = fused;
-    // MMSBM_SK_Y=1: the stream-0 E-step with Y entries (SK_Y) instead of the three-stream fused
-    // E-step (SK_U, the default).  Same-box A/B (profiles/r04j_sky_ab.txt): SK_Y does less than half
-    // SK_U's work and wins where the grid is throughput-bound (fold0 K=10, 8 samples: 78.2k vs 62.1k
-    // sample-iter/s) but loses at one sample, where both are bound by one wave's latency chain
-    // (25.1 vs 23.2 us per iteration).  The choice cannot follow B: bits must not depend on the batch.
-    const char* y = getenv("MMSBM_SK_Y");
-    const bool sky = fused && y && y[0] == '1';
-    if (sky != c->sk_y) {  // the plans hold different streams: set links again
-      DeviceGuard g(c->device);
-      for (auto& sd : c->sets) sd.release();
-      c->ws = nullptr;
-      c->ws_bytes = 0;
-    }
-    c->sk_y = sky;
   }
+  c->nact = 0;
+  apply_family(c);
   ++c->gen;
   c->attr = 0;      // the dynamic-LDS opt-ins are per kernel, and the kernels depend on K
   c->warm = false;
@@ -1903,6 +1915,10 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu < 1)
       ncu = 256;
     units_a = units_b = 15 * ncu;
+    // SK_Y (stream 0 only, the batched family): half as many, twice as long units, 7.5 per CU
+    // (fold0 K=10 x 8: 78.2k sample-iter/s at 1,920 units vs 62.2k at 3,840,
+    // profiles/r04j_sky_ab.txt)
+    if (c->sk_y) units_a = units_b = 15 * ncu / 2;
   }
   if (const char* u = getenv("MMSBM_UNITS")) {
     int a = 0, b = 0;
@@ -2181,7 +2197,7 @@ int mmsbm_loglik(mmsbm_ctx* c, int32_t which, const double* theta, const double*
     return MMSBM_OK;
   }
   if ((rc = pass_of(c)(c, PASS_LL, which, theta, pr, s))) return rc;
-  reduce_kernel<<<c->B, 256, 0, s>>>(c->partL, sd.h.n_wg_a, out);
+  reduce_kernel<<<nb_of(c), 256, 0, s>>>(c->partL, sd.h.n_wg_a, out);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -2209,6 +2225,7 @@ int mmsbm_joint_iterate(mmsbm_ctx* c, mmsbm_pairs_ctx* pairs, double* theta, dou
   mmsbm_detail_pairs_shape(pairs, &pK, &pR, &pB, &pP);
   if (pK != c->K || pR != c->R || pB != c->B || pP != c->P)
     return fail(MMSBM_ERR_INVALID, "pair context shape differs from the triplet context");
+  if (nb_of(c) != c->B) return fail(MMSBM_ERR_INVALID, "joint iterations run all B samples (mmsbm_set_active)");
   if (c->zero_degree)
     return fail(MMSBM_ERR_ZERO_DEGREE, "a gene has no train link (float division by zero)");
   if (!theta || !pr || !qr || !nth2) return fail(MMSBM_ERR_INVALID, "null pointer");
@@ -2227,6 +2244,24 @@ int mmsbm_joint_iterate(mmsbm_ctx* c, mmsbm_pairs_ctx* pairs, double* theta, dou
   c->q_out = nullptr;
   c->n_qwg = 0;
   return rc;
+}
+
+int mmsbm_set_family(mmsbm_ctx* c, int32_t family) {
+  if (!c) return fail(MMSBM_ERR_INVALID, "null context");
+  if (family != MMSBM_FAMILY_AUTO && family != MMSBM_FAMILY_SKU && family != MMSBM_FAMILY_SKY)
+    return fail(MMSBM_ERR_INVALID, "family=%d", family);
+  c->family = family;
+  apply_family(c);
+  ++c->gen;
+  return MMSBM_OK;
+}
+
+int mmsbm_set_active(mmsbm_ctx* c, int32_t n) {
+  if (!c) return fail(MMSBM_ERR_INVALID, "null context");
+  if (n < 0) return fail(MMSBM_ERR_INVALID, "active samples %d < 0", n);
+  c->nact = n >= c->B ? 0 : n;
+  ++c->gen;  // a captured graph bakes in the grids
+  return MMSBM_OK;
 }
 
 int mmsbm_set_theta_addend(mmsbm_ctx* c, const double* nth_add) {

@@ -608,7 +608,8 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// SK_Y (round 4, the default small-K E-step): ONE launch over the stream-0 slots only.  The j- and
+// SK_Y (round 4; the family for B >= 2 under MMSBM_FAMILY_AUTO, or as a driver fixes it per run with
+// mmsbm_set_family; SK_U serves one sample): ONE launch over the stream-0 slots only.  The j- and
 // k-slot sums of an observation factor through its stream-0 pivot's V table (mmsbm.hip header,
 // tests/pivot_model.py::iterate_y):
 //   sum_ah T = th_j[b] Z[b],  Z[b] = sum_h V_i[b][h] th_k[h];   sum_ab T = th_k[h] Z'[h],
@@ -938,8 +939,10 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
 
 // ------------------------------------------------------------------------------------------
 // sk_fin_kernel, grid (gene workgroups + cell workgroups + q workgroups, B), block 256.
-//   gene part: thread (g, x): X = the sum of g's X partials (gene-major: (stream, rating, row)
-//     order) (+ the joint model's pair sums); theta' = theta X / deg (:1016-1018) or, SUMS, nth = X.  SK_Y plans (ybuf set): one wave per gene; its Y entries (one contiguous
+//   gene part, SK_U plans: thread (g, x): X = the sum of g's X partials (gene-major: (stream,
+//     rating, row) order) (+ the joint model's pair sums); theta' = theta X / deg (:1016-1018)
+//     or, SUMS, nth = X.
+//   gene part, SK_Y plans (ybuf set): one wave per gene; its Y entries (one contiguous
 //     block of K-word rows, Plan::yptr) are summed by lanes l < K floor(64 / K), lane l taking
 //     words l, l + LY, ... (component l mod K), the lanes of one component then added in lane
 //     order; lane x < K adds that to its X^0 partial rows (stream 0) and updates theta.

@@ -33,7 +33,14 @@ class EMEngine:
               2: {"fused": 0, "fin": 2},
               3: {"fused": 0, "fin": 2}}
 
-    def __init__(self, K: int, P: int, B: int = 1, R: int = 2, eps: float = 1e-10, device=None):
+    FAMILIES = {None: _lib.FAMILY_AUTO, "auto": _lib.FAMILY_AUTO, "sku": _lib.FAMILY_SKU,
+                "sky": _lib.FAMILY_SKY}
+
+    def __init__(self, K: int, P: int, B: int = 1, R: int = 2, eps: float = 1e-10, device=None,
+                 family=None):
+        """family (K <= 12, include/mmsbm.h mmsbm_set_family): "sku", "sky" or None / "auto"
+        (SK_U at B = 1, SK_Y from B = 2).  A sample's bits depend on the family and on nothing
+        else, so a driver whose engines differ in B for one run fixes it (family_for_batch)."""
         if not torch.cuda.is_available():
             raise RuntimeError("EMEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.lib = _lib.load()
@@ -48,6 +55,10 @@ class EMEngine:
         _lib.check(self.lib.mmsbm_create(self.device.index, ctypes.byref(ctx)))
         self.ctx = ctx
         _lib.check(self.lib.mmsbm_set_shape(self.ctx, self.K, self.R, self.B, self.P, self.eps))
+        if family not in self.FAMILIES:
+            raise ValueError("family %r: one of sku, sky, auto" % (family,))
+        _lib.check(self.lib.mmsbm_set_family(self.ctx, self.FAMILIES[family]))
+        self.active = self.B
         self._sets = set()
         self.workspace = None
         self.theta = torch.zeros((self.B, self.P, self.K), dtype=torch.float64, device=self.device)
@@ -96,6 +107,35 @@ class EMEngine:
         self.theta.copy_(torch.from_numpy(np.ascontiguousarray(theta)))
         self.pr.copy_(torch.from_numpy(np.ascontiguousarray(pr.transpose(0, 2, 1))))
 
+    # ---------------------------------------------------------- sample slots
+    # A restart pool (restarts.run_pool) retires converged samples: it refills a slot with the next
+    # pending sample, or moves the last live slot into it and shrinks the active prefix.
+    def set_active(self, n: int):
+        """Iterate / evaluate samples [0, n) only (include/mmsbm.h mmsbm_set_active)."""
+        if not 0 < n <= self.B:
+            raise ValueError("active samples %d outside [1, %d]" % (n, self.B))
+        _lib.check(self.lib.mmsbm_set_active(self.ctx, int(n)))
+        self.active = int(n)
+
+    def upload_slot(self, b: int, theta: np.ndarray, pr: np.ndarray):
+        """One sample's theta [P][K] and pr [K][K][K][R] into slot b."""
+        th = np.asarray(theta, dtype=np.float64).reshape(self.P, self.K)
+        p = np.asarray(pr, dtype=np.float64).reshape(self.K3, self.R)
+        self.theta[b].copy_(torch.from_numpy(np.ascontiguousarray(th)))
+        self.pr[b].copy_(torch.from_numpy(np.ascontiguousarray(p.T)))
+
+    def download_slot(self, b: int):
+        """-> theta [P][K], pr [K][K][K][R] of slot b (host numpy)."""
+        th = self.theta[b].cpu().numpy()
+        pr = self.pr[b].cpu().numpy().T.reshape(self.K, self.K, self.K, self.R)
+        return th, np.ascontiguousarray(pr)
+
+    def move_slot(self, dst: int, src: int):
+        """Slot src's parameters into slot dst (a device copy: the bits travel unchanged)."""
+        if dst != src:
+            self.theta[dst].copy_(self.theta[src])
+            self.pr[dst].copy_(self.pr[src])
+
     def download(self):
         """-> theta [B][P][K], pr [B][K][K][K][R] (host numpy)."""
         th = self.theta.cpu().numpy()
@@ -129,9 +169,13 @@ class EMEngine:
         return out
 
     def loglik(self, which: int = _lib.SET_TRAIN) -> np.ndarray:
+        """[B] host array; slots outside the active prefix read NaN."""
         if which not in self._sets:
-            return np.zeros(self.B)
-        return self.loglik_async(which).cpu().numpy()
+            out = np.zeros(self.B)
+        else:
+            out = self.loglik_async(which).cpu().numpy()
+        out[self.active:] = np.nan
+        return out
 
     def predict(self, ids: np.ndarray) -> np.ndarray:
         """P(r=1) for each row of ids int32[n][3] -> [B][n] (host)."""

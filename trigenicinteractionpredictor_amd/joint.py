@@ -61,14 +61,18 @@ class JointEngine:
     (qr f64[B][R][K^2]).  One iteration = triplet accumulate, pair accumulate into the same
     ntheta, M-step of theta / pr with the joint counter, qr M-step (include/mmsbm_pairs.h)."""
 
-    def __init__(self, K: int, P: int, B: int = 1, R: int = 2, eps: float = 1e-10, device=None):
+    def __init__(self, K: int, P: int, B: int = 1, R: int = 2, eps: float = 1e-10, device=None,
+                 family="sku"):
         import ctypes
 
         import torch
 
         from .engine import EMEngine
         self._ct = ctypes
-        self.tri = EMEngine(K, P, B=B, R=R, eps=eps, device=device)
+        # the triplet half keeps one small-K kernel family for every B (the three-stream fused
+        # E-step, whose fin adds the pair sums and runs the q cells), so batched joint samples keep
+        # their one-sample bits
+        self.tri = EMEngine(K, P, B=B, R=R, eps=eps, device=device, family=family)
         self.lib, self.device = self.tri.lib, self.tri.device
         self.K, self.P, self.B, self.R, self.eps = self.tri.K, self.tri.P, self.tri.B, self.tri.R, self.tri.eps
         ctx = ctypes.c_void_p()

@@ -17,7 +17,7 @@ block still divides by its true degree, and a gene with no train link anywhere r
 ZeroDivisionError on every rank, as :1018 does.
 
 `LinkShardedEM` has the upload / iterate / loglik / download interface of `EMEngine`, so the
-restart driver's convergence loop (`restarts.run_samples`) runs it unchanged; likelihoods are
+restart driver's convergence loop (`restarts.run_pool`) runs it unchanged; likelihoods are
 summed over ranks the same way (the test links are sharded too).
 """
 from __future__ import annotations
@@ -90,6 +90,20 @@ class LinkShardedEM:
 
     def download(self):
         return self.engine.download()
+
+    # sample slots (restarts.run_pool): every rank holds the same B samples, so slot operations
+    # are local and identical on every rank
+    def upload_slot(self, b, theta, pr):
+        self.engine.upload_slot(b, theta, pr)
+
+    def download_slot(self, b):
+        return self.engine.download_slot(b)
+
+    def move_slot(self, dst, src):
+        self.engine.move_slot(dst, src)
+
+    def set_active(self, n):
+        self.engine.set_active(n)
 
     def iterate(self, n_iters: int = 1):
         for _ in range(int(n_iters)):

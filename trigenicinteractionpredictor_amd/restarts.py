@@ -61,49 +61,163 @@ class SampleResult:
     pr: np.ndarray = field(default=None, repr=False)
 
 
+def family_for_batch(batch: int) -> str:
+    """The small-K kernel family for a run configured with `batch` samples per engine
+    (include/mmsbm.h mmsbm_set_family): SK_Y from 2 (the throughput winner), SK_U for one sample
+    (the latency winner).  Fixed per run, so a ragged last batch, a rank with a smaller share or a
+    shrinking pool gives its samples the same bits as the full batches."""
+    return "sky" if int(batch) >= 2 else "sku"
+
+
+def next_stop(it: int, iterations: int, fcheck: int, bcheck: int):
+    """(iterations to run from `it` to the next stop, whether that stop is a check): the reference
+    checks after make_iteration #c when c % fcheck == 0 and c > bcheck (:1268), and a sample ends
+    after `iterations` iterations (:1264)."""
+    c = max(it, bcheck + 1)
+    c = -(-c // fcheck) * fcheck
+    if c < iterations:
+        return c + 1 - it, True
+    return iterations - it, False
+
+
+@dataclass
+class PoolStats:
+    """What a pool run cost: slot_iterations = sum over iterate calls of (iterations x live
+    slots); sample_iterations = the iterations the samples needed (sum of SampleResult.iterations);
+    calls = engine.iterate calls; refills = slots handed to a pending sample; shrinks = active-prefix
+    reductions."""
+    slot_iterations: int = 0
+    sample_iterations: int = 0
+    calls: int = 0
+    refills: int = 0
+    shrinks: int = 0
+
+
+def run_pool(engine, states, iterations=10000, fcheck=25, bcheck=100, keep_params=False,
+             on_done=None, stats: PoolStats = None):
+    """Drive samples through a B-slot engine with the reference's per-sample loop (:1259-1279),
+    retiring each sample at convergence (or after `iterations`) and handing its slot to the next
+    pending one at once, as the reference's process starts its next sample (:1253-1279) and
+    run.sh keeps every core busy (src/run.sh:12,16,45).
+
+    `states` yields (sample id, theta [P][K], pr [K][K][K][R]) in sample order; it is consumed
+    lazily, one sample per free slot, so initial states are drawn in sample order (:1260) whenever
+    they are drawn.  Every slot keeps its own iteration count and check schedule; one engine.iterate
+    call advances all live slots to the nearest stop of any of them.  When nothing is pending a
+    finished slot takes the last live slot's parameters (a device copy) and the active prefix
+    shrinks (engine.set_active), so no GPU time goes to finished samples.  A sample's bits do not
+    depend on its slot or its batch-mates (one kernel family per run), so every result equals the
+    sequential run's.  `engine` provides B, upload_slot, download_slot, move_slot, set_active,
+    iterate, loglik.  on_done(result) is called as each sample finishes; returns the results in
+    finishing order."""
+    B = engine.B
+    src = iter(states)
+    slots = [None] * B       # per slot: [sample id, iterations run, previous check likelihood]
+    pending_done = False
+
+    def fill(b):
+        nonlocal pending_done
+        if pending_done:
+            return False
+        try:
+            sid, th, pr = next(src)
+        except StopIteration:
+            pending_done = True
+            return False
+        engine.upload_slot(b, th, pr)
+        slots[b] = [sid, 0, None]
+        return True
+
+    n_act = 0
+    while n_act < B and fill(n_act):
+        n_act += 1
+    if n_act == 0:
+        return []
+    engine.set_active(n_act)
+    like = engine.loglik(TRAIN)
+    for b in range(n_act):
+        slots[b][2] = float(like[b])
+    out = []
+    stats = stats if stats is not None else PoolStats()
+    while n_act:
+        stops = [next_stop(slots[b][1], iterations, fcheck, bcheck) for b in range(n_act)]
+        n = min(st[0] for st in stops)
+        if n > 0:
+            engine.iterate(n)
+            stats.calls += 1
+            stats.slot_iterations += n * n_act
+        for b in range(n_act):
+            slots[b][1] += n
+        like = held = None
+        finished = []                  # (slot, converged, likelihood)
+        for b in range(n_act):
+            steps, check = stops[b]
+            if steps != n:
+                continue
+            if check:
+                if like is None:
+                    like = engine.loglik(TRAIN)
+                if math.fabs((like[b] - slots[b][2]) / slots[b][2]) < 0.01:
+                    finished.append((b, True, float(like[b])))
+                    continue
+                slots[b][2] = float(like[b])
+            if slots[b][1] >= iterations:
+                if like is None:
+                    like = engine.loglik(TRAIN)
+                finished.append((b, False, float(like[b])))
+        if not finished:
+            continue
+        held = engine.loglik(TEST)
+        for b, conv, L in finished:
+            th = pr = None
+            if keep_params:
+                th, pr = engine.download_slot(b)
+            r = SampleResult(slots[b][0], slots[b][1], conv, L, float(held[b]), th, pr)
+            stats.sample_iterations += r.iterations
+            out.append(r)
+            if on_done is not None:
+                on_done(r)
+            slots[b] = None
+        refilled = []
+        for b, _, _ in finished:       # slot order = the order pending samples are drawn in
+            if fill(b):
+                refilled.append(b)
+                stats.refills += 1
+        live = [b for b in range(n_act) if slots[b] is not None]
+        if len(live) < n_act:          # nothing pending: compact the live slots to the front
+            for e in range(len(live)):
+                if slots[e] is None:
+                    h = max(b for b in range(e + 1, n_act) if slots[b] is not None)
+                    engine.move_slot(e, h)
+                    slots[e], slots[h] = slots[h], None
+                    refilled = [e if x == h else x for x in refilled]
+            n_act = len(live)
+            stats.shrinks += 1
+            if n_act:
+                engine.set_active(n_act)
+        if refilled:
+            like = engine.loglik(TRAIN)
+            for b in refilled:
+                slots[b][2] = float(like[b])
+    return out
+
+
 def run_samples(engine, sample_ids, thetas, prs, iterations=10000, fcheck=25, bcheck=100,
                 keep_params=False):
-    """Drive the batched engine with the reference's per-sample convergence rule.
+    """The batched engine over exactly these samples (one slot each) with the reference's
+    per-sample convergence rule; results in sample order.  See run_pool."""
+    res = run_pool(engine, zip(sample_ids, thetas, prs), iterations, fcheck, bcheck, keep_params)
+    order = {s: i for i, s in enumerate(sample_ids)}
+    return sorted(res, key=lambda r: order[r.sample])
 
-    `engine` provides upload(thetas, prs), iterate(n), loglik(which) -> [B], download().
-    """
-    B = len(sample_ids)
-    engine.upload(np.stack(thetas), np.stack(prs))
-    like0 = np.array(engine.loglik(TRAIN), dtype=np.float64)
-    done = [None] * B
-    it = 0
-    while it < iterations and any(d is None for d in done):
-        # next check iteration (reference checks right after make_iteration #it)
-        nxt = it
-        while nxt < iterations and not (nxt % fcheck == 0 and nxt > bcheck):
-            nxt += 1
-        n = min(nxt, iterations - 1) - it + 1
-        engine.iterate(n)
-        it += n
-        if it - 1 == nxt and nxt < iterations:
-            like = np.array(engine.loglik(TRAIN), dtype=np.float64)
-            snap = None
-            for s in range(B):
-                if done[s] is not None:
-                    continue
-                if math.fabs((like[s] - like0[s]) / like0[s]) < 0.01:
-                    if snap is None:
-                        snap = engine.download() if keep_params else (None, None)
-                        held = np.array(engine.loglik(TEST), dtype=np.float64)
-                    done[s] = SampleResult(sample_ids[s], it, True, float(like[s]), float(held[s]),
-                                           None if snap[0] is None else snap[0][s],
-                                           None if snap[1] is None else snap[1][s])
-                like0[s] = like[s]
-    if any(d is None for d in done):
-        like = np.array(engine.loglik(TRAIN), dtype=np.float64)
-        held = np.array(engine.loglik(TEST), dtype=np.float64)
-        snap = engine.download() if keep_params else (None, None)
-        for s in range(B):
-            if done[s] is None:
-                done[s] = SampleResult(sample_ids[s], it, False, float(like[s]), float(held[s]),
-                                       None if snap[0] is None else snap[0][s],
-                                       None if snap[1] is None else snap[1][s])
-    return done
+
+def stream_states(model, K: int, samples, mine=None):
+    """(sample, theta, pr) for the samples in `mine` (default: all), drawing every sample's initial
+    state from the one stdlib stream in `samples` order (:1260), lazily."""
+    for s in samples:
+        model.initialize_parameters(K)
+        if mine is None or s in mine:
+            yield s, np.array(model._theta, dtype=np.float64), np.array(model._pr, dtype=np.float64)
 
 
 def gather_results(results: list[SampleResult], n_samples: int, group=None, device=None):
@@ -130,9 +244,11 @@ def gather_results(results: list[SampleResult], n_samples: int, group=None, devi
 
 
 def run_restarts(model, K, n_samples, seed, iterations=10000, fcheck=25, bcheck=100,
-                 engine_factory=None, group=None, device=None):
-    """Shard `n_samples` restarts over the process group (or run all locally), drive them,
-    and return every sample's result on every rank (sorted by sample id)."""
+                 engine_factory=None, group=None, device=None, batch=None):
+    """Shard `n_samples` restarts over the process group (or run all locally), drive them in one
+    pool per rank (run_pool: `batch` slots, default the rank's whole share) and return every
+    sample's result on every rank (sorted by sample id).  The kernel family follows `batch`, or
+    n_samples when no batch is given, so the results do not depend on the world size."""
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
     world = dist.get_world_size(group) if dist_on else 1
@@ -144,13 +260,16 @@ def run_restarts(model, K, n_samples, seed, iterations=10000, fcheck=25, bcheck=
         if engine_factory is None:
             from .engine import EMEngine
             from .layout import links_to_arrays
+            family = family_for_batch(batch if batch else n_samples)
 
             def engine_factory(B):
-                eng = EMEngine(K, model.P, B=B, R=model.R, eps=model.eps, device=device)
+                eng = EMEngine(K, model.P, B=B, R=model.R, eps=model.eps, device=device, family=family)
                 eng.set_links(TRAIN, *links_to_arrays(model.links, model.R))
                 eng.set_links(TEST, *links_to_arrays(model.test_links, model.R))
                 return eng
-        local = run_samples(engine_factory(len(ids)), ids, thetas, prs, iterations, fcheck, bcheck)
+        slots = min(batch or len(ids), len(ids))
+        local = run_pool(engine_factory(slots), zip(ids, thetas, prs), iterations, fcheck, bcheck)
+        local.sort(key=lambda r: r.sample)
     if not dist_on:
         return local
     return gather_results(local, n_samples, group=group, device=device)

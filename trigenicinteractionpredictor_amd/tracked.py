@@ -32,16 +32,22 @@ class Version:
 
 
 class TrackedRow(list):
-    """The rating counts [n_0, n_1, ...] of one link; edits bump the owner's counter."""
+    """The rating counts [n_0, n_1, ...] of one link; edits bump the counter of every table that
+    holds this row object (one list shared by two tables, as the same list object in two of the
+    reference's dicts would be, is seen by both)."""
     __slots__ = ("_v",)
 
     def __init__(self, it=(), version: Version = None):
         super().__init__(it)
-        self._v = version
+        self._v = () if version is None else (version,)
+
+    def _own(self, version: Version):
+        if all(v is not version for v in self._v):
+            self._v += (version,)
 
     def _bump(self):
-        if self._v is not None:
-            self._v.bump()
+        for v in self._v:
+            v.bump()
 
     def __setitem__(self, i, x):
         super().__setitem__(i, x)
@@ -107,7 +113,11 @@ class TrackedLinks(dict):
     own edits, so the table keeps `d` as its source and shares the row objects with it: `d`'s
     values are replaced by the table's TrackedRow rows (equal lists), so `d[k][r] += 1` is seen at
     once; every edit made through the table is applied to `d` too; and a key added to or removed
-    from `d` itself is picked up by `resync()` (what `Model.links_changed()` calls)."""
+    from `d` itself is picked up by `resync()` (what `Model.links_changed()` calls).  A dict may
+    back several tables (two Models, or `links` and `test_links`): rows already tracked are
+    reused, not replaced, and notify every table holding them, so `d[k][r] += 1` reaches all of
+    them; a key added or removed through one table reaches `d`, and the others pick it up at
+    their own `resync()`, like a key added to `d` directly."""
 
     def __init__(self, src=None, version: Version = None, alias: dict = None):
         super().__init__()
@@ -136,7 +146,8 @@ class TrackedLinks(dict):
 
     def _row(self, v):
         if isinstance(v, list):
-            if isinstance(v, TrackedRow) and v._v is self.version:
+            if isinstance(v, TrackedRow):
+                v._own(self.version)
                 return v
             return TrackedRow(v, self.version)
         return v
