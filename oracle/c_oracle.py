@@ -36,6 +36,9 @@ def lib():
         L.oracle_make_iteration.restype = ctypes.c_int
         L.oracle_make_iteration.argtypes = [ctypes.c_int64, P_i32, P_i32, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_double, P_f64, P_f64]
+        L.oracle_accumulate.restype = None
+        L.oracle_accumulate.argtypes = [ctypes.c_int64, P_i32, P_i32, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_double, P_f64, P_f64, P_f64, P_f64]
         L.oracle_predict.restype = None
         L.oracle_predict.argtypes = [ctypes.c_int64, P_i32, ctypes.c_int, ctypes.c_int,
                                      P_f64, P_f64, P_f64]
@@ -82,6 +85,20 @@ def make_iteration(ids, counts, theta, pr, eps=1e-10):
     if rc != 0:
         raise ZeroDivisionError("float division by zero")
     return theta, pr
+
+
+def accumulate(ids, counts, theta, pr, eps=1e-10):
+    """The per-link sums of :986-1012 over these links -> (nth [P][K], npr [K][K][K][R]); the
+    C loop releases the GIL, so disjoint link blocks can run on threads."""
+    theta = np.ascontiguousarray(theta, dtype=np.float64)
+    pr = np.ascontiguousarray(pr, dtype=np.float64)
+    P, K = theta.shape
+    R = counts.shape[1]
+    nth = np.zeros((P, K), dtype=np.float64)
+    npr = np.zeros(pr.shape, dtype=np.float64)
+    lib().oracle_accumulate(ids.shape[0], np.ascontiguousarray(ids, dtype=np.int32),
+                            np.ascontiguousarray(counts, dtype=np.int32), P, K, R, eps, theta, pr, nth, npr)
+    return nth, npr
 
 
 def predict(ids, theta, pr):

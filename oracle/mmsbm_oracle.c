@@ -80,6 +80,18 @@ static void tri_accumulate(int64_t E, const int32_t *ids, const int32_t *counts,
     }
 }
 
+/* The accumulation half of make_iteration (:986-1012) over a subset of the links, adding into
+ * nth[P][K] and npr[K^3][R] (zeroed by the caller): the sums a gene's theta' needs (:1016-1018)
+ * are complete when every link holding the gene is in the subset (tests: config-5 genes checked
+ * at full size, with the degree counted over all links). */
+void oracle_accumulate(int64_t E, const int32_t *ids, const int32_t *counts, int P, int K, int R,
+                       double eps, const double *theta, const double *pr, double *nth, double *npr)
+{
+    int64_t *deg = calloc((size_t)P, sizeof(int64_t));
+    tri_accumulate(E, ids, counts, K, R, eps, theta, pr, nth, npr, deg);
+    free(deg);
+}
+
 /* cells[n][R] <- cells / (eps + sum_r cells), :1021-1028 */
 static void normalise_cells(int64_t n, int R, double eps, double *cells)
 {

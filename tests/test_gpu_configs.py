@@ -306,6 +306,41 @@ def test_config5_subfold_full_iteration_against_oracle(c5):
     eng.close()
 
 
+def test_config5_full_iteration_theta_rows_against_oracle(c5):
+    """Config 5 at full size (10M links, 50k genes, K=30): after ONE full GPU iteration, theta'
+    of 200 genes against the C oracle.  The genes: the 20 of highest degree
+    (the longest pivot runs, split over units, waves and workgroups, their partial rows merged)
+    and 180 drawn at random.  The oracle accumulates :986-1012 over every link holding one of them
+    (16 link blocks on threads, summed in block order) and divides by the degree over ALL links
+    (:1016-1018), which is exactly theta' for those genes."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import c_oracle
+    from trigenicinteractionpredictor_amd.linkshard import train_degree
+    P, ids, counts, th, pr = c5
+    deg = train_degree(ids, P)
+    top = np.argsort(-deg, kind="stable")[:20]
+    rest = np.setdiff1d(np.arange(P), top)
+    pick = np.concatenate([top, np.random.default_rng(11).choice(rest, 180, replace=False)])
+    sel = np.zeros(P, dtype=bool)
+    sel[pick] = True
+    mask = sel[ids].any(axis=1)
+    sub_ids, sub_counts = ids[mask], counts[mask]
+    eng = _c5_engine(c5)
+    eng.iterate(1)
+    t_gpu = eng.theta[0].cpu().numpy()[pick]
+    eng.close()
+    blocks = np.array_split(np.arange(sub_ids.shape[0]), 16)
+    with ThreadPoolExecutor(16) as ex:
+        parts = list(ex.map(lambda b: c_oracle.accumulate(sub_ids[b], sub_counts[b], th, pr)[0], blocks))
+    nth = parts[0]
+    for part in parts[1:]:
+        nth = nth + part
+    want = nth[pick] / deg[pick, None]
+    assert sub_ids.shape[0] > 100_000 and deg[top].min() > deg.mean()
+    np.testing.assert_allclose(t_gpu, want, rtol=RTOL, atol=ATOL)
+
+
 def test_restart_driver_on_gpu_matches_oracle_driver(tmp_path):
     """restarts.run_samples on the batched GPU engine: the same per-sample iterations, convergence
     and likelihoods as the driver on the oracle engine (:1253-1279 per sample)."""

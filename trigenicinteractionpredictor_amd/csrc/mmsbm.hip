@@ -1074,6 +1074,243 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(4))) 
 }
 
 // ------------------------------------------------------------------------------------------
+// gm_kernel (round 5; launch 2 of a large-K iteration): both contractions of the stream-0 partial
+// rows in ONE pass over them, as two GEMMs on v_mfma_f64_16x16x4f64:
+//   X_q[a]       = sum_cell M_q[cell] p_r[a][cell]        per partial row q  (-> xrow[CS][B][n_prows][K];
+//                  upd sums a gene's rows, so x0_g = sum_r sum_{q of (r, g)} X_q, :1009 / :1016)
+//   S_w[a][cell] = sum_{q in w} th_g(q)[a] M_q[cell]       per part w         (-> spart, :1012)
+// grid (n_sp x CS, B), block 512.  Part w = the rows [q0, q1) of one rating (Plan::sp_desc, 128 rows
+// a part); its cells are split into CS groups of whole 64-cell chunks, one workgroup each (CS = 2
+// from 9 chunks, K >= 24: the S accumulators of one group then fit the registers of two workgroups
+// per CU).  A workgroup walks its rows in tiles of 64 and, in a tile, its chunks: the chunk's M tile
+// (64 x 64, from HBM), p_r's 64 cells of every a (L2) and the tile's theta rows sit in LDS; every M
+// word is read from HBM once and feeds both products.  Wave wv owns one 16 x 16 X tile (row tile,
+// a tile) of the row tile, over the group's chunks (its part of X_q: upd adds the CS groups), and
+// one S tile (cell tile, a tile) of every chunk of the group, over all the part's rows (K <= 16:
+// 4 tiles each for 8 waves, so two waves split each tile's k-steps and add their parts in wave
+// order).  The next chunk's loads are in flight during the current chunk's MFMAs (register
+// staging, one LDS buffer).  LDS (72 KB): M tile [64 rows][64] and p chunk [32 a][64], columns
+// XOR-swizzled by the row (gm_swz: the X operand reads 16 rows x 2 cells, the S operand 2 rows x 16
+// cells, both conflict-free ds_read_b64; addresses formed per k-step, not hoisted, so they take no
+// registers), theta tile [64][48] (stride = 16 mod 32 doubles).  Replaces round 4's gene_kernel x0
+// workgroups (16 genes each, all of p_r re-read from L2 per workgroup) and gene_sy's S workgroups
+// (a second read of every partial row).
+// ------------------------------------------------------------------------------------------
+#ifndef MMSBM_GM
+#define MMSBM_GM 1
+#endif
+// gm_kernel occupancy hint: 4 waves per SIMD (<= 128 VGPRs, two 72 KB workgroups per CU) where
+// that does not spill (K <= 16); above, the S accumulators and staging take up to 254 VGPRs and the
+// hint is free (one workgroup per CU; 128 spilled 58-120 VGPRs at K = 20-32)
+template <int K>
+struct GM {
+  static constexpr int K2 = K * K;
+  static constexpr int NA = (K + 15) / 16;   // 16-wide a tiles
+  static constexpr int AP = 16 * NA;
+  static constexpr int RT = 64, CW = 64;     // rows per row tile, cells per chunk
+  static constexpr int NCH = (K2 + CW - 1) / CW;
+  static constexpr int CS = NCH > 8 ? 2 : 1;              // cell groups (workgroups) per part
+  static constexpr int CPG = (NCH + CS - 1) / CS;         // chunks per group
+  static constexpr int TST = AP == 32 ? 48 : 16;  // theta tile row stride (= 16 mod 32 doubles)
+  static constexpr int XT = 4 * NA, XK = 8 / XT;  // X tiles per row tile, k-splits per tile
+  static constexpr int ST = 4 * NA, SK = 8 / ST;  // S tiles per chunk, row splits per tile
+  static constexpr int MW = K2 % 2 == 0 ? 2 : 1;  // staging width (a row starts 16-B aligned)
+  static constexpr int NM = RT * CW / MW / 512;   // M staging loads per thread
+  static constexpr int NP = (AP * CW / MW + 511) / 512;
+  static constexpr int NTH = RT * AP / 512;       // theta staging loads per thread
+  static constexpr int LDS = (RT * CW + AP * CW + RT * TST) * 8;
+  static constexpr int WPE = K <= 16 ? 4 : 1;
+  static_assert(XT * XK == 8 && ST * SK == 8, "gm: 8 waves");
+  static_assert(RT * CW % (MW * 512) == 0 && RT * AP % 512 == 0, "gm staging");
+};
+
+// column swizzle of the 64-wide LDS tiles: bit 4 <- row bit 0, bits 1-3 <- row bits 1-3
+__device__ __forceinline__ int gm_swz(int r) { return ((r & 1) << 4) | (((r >> 1) & 7) << 1); }
+
+template <int K>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE))) void gm_kernel(const double* __restrict__ theta, const double* __restrict__ pr,
+                                                  const double* __restrict__ prows,
+                                                  const int* __restrict__ prow_gene,
+                                                  const int* __restrict__ sp_desc, double* __restrict__ xrow,
+                                                  double* __restrict__ spart, int P, int R, long long n_prows,
+                                                  int n_sp, long long xgs) {
+  using G = GM<K>;
+  constexpr int K2 = G::K2, K3 = K * K * K, CW = G::CW, RT = G::RT, TST = G::TST, AP = G::AP;
+  extern __shared__ __attribute__((aligned(16))) double gsm[];
+  double* Ml = gsm;                  // [RT][CW] swizzled
+  double* Pt = gsm + RT * CW;        // [AP][CW] swizzled
+  double* Tl = Pt + AP * CW;         // [RT][TST]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = blockIdx.x / G::CS, grp = blockIdx.x % G::CS, b = blockIdx.y;
+  const int cb = grp * G::CPG;       // the group's first chunk
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int* d = sp_desc + 3 * w;
+  const int r = d[0], q0 = d[1], q1 = d[2];
+  const double* __restrict__ th = theta + (size_t)b * P * K;
+  const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
+  const double* __restrict__ mb = prows + (size_t)b * n_prows * K2;
+  double* __restrict__ xb = xrow + (size_t)grp * xgs + (size_t)b * n_prows * K;  // xgs: a group's X rows
+  // this wave's X tile (row tile xr, a tile xa, k-split xk) and S tile (cell tile sc, a tile sa,
+  // row split sk) of every chunk
+  const int xt = wv % G::XT, xk = wv / G::XT, xr = xt % 4, xa = xt / 4;
+  const int st = wv % G::ST, sk = wv / G::ST, sc = st % 4, sa = st / 4;
+  constexpr int XKS = 16 / G::XK, SKS = 16 / G::SK;  // k-steps per split
+  d4v sacc[G::CPG];
+#pragma unroll
+  for (int c = 0; c < G::CPG; ++c) sacc[c] = d4v{0.0, 0.0, 0.0, 0.0};
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  using MV = typename std::conditional<G::MW == 2, d2v, double>::type;
+
+  // staging of chunk c of the row tile starting at row qt: M words (rows past q1 and cells past
+  // K2 load a clamped address and are zeroed), p_r's cells of the chunk for every a
+  auto load_m = [&](int qt, int c, MV (&mv)[G::NM]) {
+#pragma unroll
+    for (int u = 0; u < G::NM; ++u) {
+      const int idx = tid + 512 * u, row = idx / (CW / G::MW), col = G::MW * (idx % (CW / G::MW));
+      const int q = qt + row, cell = c * CW + col;
+      const bool ok = q < q1 && cell < K2;
+      const MV v = *reinterpret_cast<const MV*>(mb + (size_t)(ok ? q : q0) * K2 + (ok ? cell : 0));
+      mv[u] = ok ? v : MV{};
+    }
+  };
+  auto load_p = [&](int c, MV (&pv)[G::NP]) {
+#pragma unroll
+    for (int u = 0; u < G::NP; ++u) {
+      const int idx = tid + 512 * u, a = idx / (CW / G::MW), col = G::MW * (idx % (CW / G::MW));
+      const int cell = c * CW + col;
+      const bool ok = idx < AP * CW / G::MW && a < K && cell < K2;
+      const MV v = *reinterpret_cast<const MV*>(p + (ok ? (size_t)a * K2 + cell : 0));
+      pv[u] = ok ? v : MV{};
+    }
+  };
+  auto store_mp = [&](const MV (&mv)[G::NM], const MV (&pv)[G::NP]) {
+#pragma unroll
+    for (int u = 0; u < G::NM; ++u) {
+      const int idx = tid + 512 * u, row = idx / (CW / G::MW), col = G::MW * (idx % (CW / G::MW));
+      *reinterpret_cast<MV*>(Ml + row * CW + (col ^ gm_swz(row))) = mv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < G::NP; ++u) {
+      const int idx = tid + 512 * u, a = idx / (CW / G::MW), col = G::MW * (idx % (CW / G::MW));
+      if (idx < AP * CW / G::MW) *reinterpret_cast<MV*>(Pt + a * CW + (col ^ gm_swz(a))) = pv[u];
+    }
+  };
+  auto load_t = [&](int qt, double (&tv)[G::NTH]) {
+#pragma unroll
+    for (int u = 0; u < G::NTH; ++u) {
+      const int idx = tid + 512 * u, row = idx / AP, a = idx % AP;
+      const int q = qt + row;
+      const bool ok = q < q1 && a < K;
+      const int g = prow_gene[ok ? q : q0];
+      const double v = th[(size_t)g * K + (ok ? a : 0)];
+      tv[u] = ok ? v : 0.0;
+    }
+  };
+  auto store_t = [&](const double (&tv)[G::NTH]) {
+#pragma unroll
+    for (int u = 0; u < G::NTH; ++u) {
+      const int idx = tid + 512 * u;
+      Tl[(idx / AP) * TST + idx % AP] = tv[u];
+    }
+  };
+  // per-lane LDS bases and swizzles of the operands (the k-step's address is formed in the loop)
+  const int xrow_l = 16 * xr + l15, xa_l = 16 * xa + l15;
+  const int xsw_m = gm_swz(xrow_l), xsw_p = gm_swz(xa_l);
+  const double* xm = Ml + xrow_l * CW;
+  const double* xp = Pt + xa_l * CW;
+  const double* sT = Tl + 16 * sa + l15;
+  const int scell = 16 * sc + l15;
+
+  MV mv[G::NM], pv[G::NP];
+  double tv[G::NTH];
+  if (q0 < q1) {
+    load_t(q0, tv);
+    load_m(q0, cb, mv);
+    load_p(cb, pv);
+  }
+  for (int qt = q0; qt < q1; qt += RT) {
+    d4v xacc = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < G::CPG; ++i) {
+      const int c = cb + i;
+      if (c >= G::NCH) break;  // (uniform: the last group may hold fewer chunks)
+      __syncthreads();  // the previous chunk's reads of the LDS tiles are done
+      store_mp(mv, pv);
+      if (i == 0) store_t(tv);
+      __syncthreads();
+      // next chunk (or the next row tile's first chunk and theta rows) in flight
+      if (i + 1 < G::CPG && c + 1 < G::NCH) {
+        load_m(qt, c + 1, mv);
+        load_p(c + 1, pv);
+      } else if (qt + RT < q1) {
+        load_m(qt + RT, cb, mv);
+        load_p(cb, pv);
+        load_t(qt + RT, tv);
+      }
+      // X tile: rows 16 xr + i, a 16 xa + j; k = the chunk's cells
+#pragma unroll 4
+      for (int s = xk * XKS; s < (xk + 1) * XKS; ++s) {
+        const int cell = 4 * s + l4;
+        xacc = mfma16(xm[cell ^ xsw_m], xp[cell ^ xsw_p], xacc);
+      }
+      // S tile: a 16 sa + i, cells 16 sc + j of the chunk; k = the tile's rows
+#pragma unroll 4
+      for (int s = sk * SKS; s < (sk + 1) * SKS; ++s) {
+        const int row = 4 * s + l4;
+        sacc[i] = mfma16(sT[row * TST], Ml[row * CW + (scell ^ gm_swz(row))], sacc[i]);
+      }
+    }
+    // X rows of this tile: the k-splits' parts added in wave order (XK = 2: through LDS)
+    if constexpr (G::XK == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * xr + l4 + 4 * i, a = 16 * xa + l15;
+        if (qt + row < q1 && a < K) xb[(size_t)(qt + row) * K + a] = xacc[i];
+      }
+    } else {
+      __syncthreads();  // Ml is free: park split 1's parts there
+      if (xk == 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ml[(xt * 4 + i) * 64 + lane] = xacc[i];
+      __syncthreads();
+      if (xk == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 16 * xr + l4 + 4 * i, a = 16 * xa + l15;
+          const double v = xacc[i] + Ml[(xt * 4 + i) * 64 + lane];
+          if (qt + row < q1 && a < K) xb[(size_t)(qt + row) * K + a] = v;
+        }
+    }
+  }
+  // the part's S partial over the group's cells: the row splits' parts added in wave order
+  double* __restrict__ out = spart + ((size_t)b * n_sp + w) * K3;
+  if constexpr (G::SK == 2) __syncthreads();
+#pragma unroll
+  for (int i = 0; i < G::CPG; ++i) {
+    const int c = cb + i;
+    if (c >= G::NCH) break;
+    if constexpr (G::SK == 2) {
+      if (sk == 1)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Ml[(st * 4 + e) * 64 + lane] = sacc[i][e];
+      __syncthreads();
+      if (sk == 0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc[i][e] += Ml[(st * 4 + e) * 64 + lane];
+      __syncthreads();
+    }
+    if (sk == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int a = 16 * sa + l4 + 4 * e, cell = c * CW + 16 * sc + l15;
+        if (a < K && cell < K2) out[(size_t)a * K2 + cell] = sacc[i][e];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // upd_kernel (launch 3), grid (theta workgroups + cell workgroups + q workgroups, B), block 512:
 //   theta workgroups: thread (g, a): X = x0 + ysum (+ the joint model's pair sums);
 //     theta' = theta X / deg (:1016-1018), or SUMS: nth = X
@@ -1089,7 +1326,8 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
     const double* __restrict__ ysum, const double* __restrict__ spart, const int* __restrict__ deg,
     SpRange spr, int P, int R, int n_sp, int n_th_wg, double eps, double* __restrict__ nth_out,
     double* __restrict__ S_out, const double* __restrict__ nth_add, const double* __restrict__ q_part,
-    double* __restrict__ q_out, int n_qwg) {
+    double* __restrict__ q_out, int n_qwg, const double* __restrict__ xrow, const int* __restrict__ prow_ptr,
+    long long n_prows, long long xgs) {
   constexpr int K2 = K * K, K3 = K * K * K;
   constexpr int NCW = (K3 + 63) / 64, NPART = UPD_NT / 64;
   __shared__ double red[MAX_R * NPART * 64];
@@ -1098,7 +1336,22 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
     const long long item = (long long)w * UPD_NT + tid;
     if (item >= (long long)P * K) return;  // no barrier in this branch
     const size_t o = (size_t)b * P * K + item;
-    double X = x0[o] + ysum[o];
+    double X;
+    if (xrow) {  // gm_kernel: the gene's X rows, rating then row order, cell groups in order
+      const int g = (int)(item / K), a = (int)(item % K);
+      const double* __restrict__ xb = xrow + (size_t)b * n_prows * K + a;
+      X = 0.0;
+      for (int r = 0; r < R; ++r)
+        for (int q = prow_ptr[(size_t)r * (P + 1) + g], qe = prow_ptr[(size_t)r * (P + 1) + g + 1]; q < qe; ++q) {
+          double x = xb[(size_t)q * K];
+#pragma unroll
+          for (int h = 1; h < GM<K>::CS; ++h) x += xb[h * xgs + (size_t)q * K];
+          X += x;
+        }
+      X += ysum[o];
+    } else {
+      X = x0[o] + ysum[o];
+    }
     if (nth_add) X += nth_add[o];
     if constexpr (SUMS) nth_out[o] = X;
     else theta[o] = theta[o] * X / (double)deg[item / K];
@@ -1386,6 +1639,9 @@ struct mmsbm_ctx {
   // large-K gene kernel as two launches: x0 workgroups, then S + Y workgroups (gene_sy_kernel) at
   // their own LDS and VGPR budget; MMSBM_GSPLIT=0: one launch (measurement)
   bool gsplit = true;
+  // large-K M-step contractions in gm_kernel (round 5); MMSBM_GM=0: round 4's gene kernel (measurement)
+  bool gm = MMSBM_GM != 0;
+  double* xrows = nullptr;       // gm_kernel's X rows [B][n_prows][K]
   hipStream_t ys = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   const double *g_theta = nullptr, *g_pr = nullptr;
@@ -1399,7 +1655,7 @@ namespace {
 inline int nb_of(const mmsbm_ctx* c) { return c->nact > 0 && c->nact < c->B ? c->nact : c->B; }
 
 struct WsLayout {
-  size_t cbuf, prows, spart, gx, partL, nth, S, total;
+  size_t cbuf, prows, spart, gx, partL, nth, S, xrows, total;
 };
 
 WsLayout ws_layout(const mmsbm_ctx* c) {
@@ -1445,6 +1701,8 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   off += align_up(B * (size_t)c->P * c->K * 8);
   L.S = off;
   off += align_up(B * c->R * K3 * 8);
+  L.xrows = off;  // gm_kernel's X rows: two cell groups at most (GM<K>::CS)
+  off += align_up(2 * B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
   L.total = off;
   return L;
 }
@@ -1498,6 +1756,17 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
       const long long nyb = ((long long)c->P * K + 255) / 256;
       ysum_kernel<K><<<dim3((unsigned)nyb, nb_of(c)), 256, 0, c->ys>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
       HIP_TRY(hipGetLastError());
+    }
+    if (c->gm) {  // round 5: gm_kernel (X rows + S partials in one pass), then the Y sums
+      if ((rc = lds_opt_in(c, 10, &gm_kernel<K>, GM<K>::LDS))) return rc;
+      gm_kernel<K><<<dim3(std::max(h.n_sp, 1) * GM<K>::CS, nb_of(c)), 512, GM<K>::LDS, s>>>(
+          theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, h.n_prows,
+          std::max(h.n_sp, 1), (long long)c->B * h.n_prows * K);
+      HIP_TRY(hipGetLastError());
+      const long long nyb = ((long long)c->P * K + 255) / 256;
+      ysum_kernel<K><<<dim3((unsigned)nyb, nb_of(c)), 256, 0, s>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
+      HIP_TRY(hipGetLastError());
+      return MMSBM_OK;
     }
     // two launches from K = 24 (K=30 gene 1,778 -> 1,745 us, profiles/r04w_gsplit_ab.txt); at
     // K = 20-23 two gene workgroups share a CU and the single launch, whose S and Y workgroups
@@ -1558,14 +1827,16 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   const size_t pk = (size_t)c->B * c->P * K;
   // joint model: the q cells (qr M-step from the pair launch's S2 partials), theta update only
   const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
+  const double* xr = c->gm ? c->xrows : nullptr;  // gm_kernel's X rows, or gene_kernel's x0
   if (sums)
     upd_kernel<K, true><<<dim3(nthw + ncw, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
-        nth, S, c->nth_add, nullptr, nullptr, 0);
+        nth, S, c->nth_add, nullptr, nullptr, 0, xr, sd.prow_ptr, h.n_prows, (long long)c->B * h.n_prows * K);
   else
     upd_kernel<K, false><<<dim3(nthw + ncw + nqc, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
-        nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg);
+        nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg, xr, sd.prow_ptr, h.n_prows,
+        (long long)c->B * h.n_prows * K);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -1792,6 +2063,7 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   if (const char* gi = getenv("MMSBM_GRAPH")) c->graph_iters = std::max(0, atoi(gi));
   if (const char* ysp = getenv("MMSBM_YSPLIT")) c->ysplit = ysp[0] != '0';
   if (const char* gsp = getenv("MMSBM_GSPLIT")) c->gsplit = gsp[0] != '0';
+  if (const char* gme = getenv("MMSBM_GM")) c->gm = gme[0] != '0';
   if (MMSBM_STAMP && getenv("MMSBM_STAMP")) {
     DeviceGuard g(device);
     const size_t bytes = sizeof(unsigned long long) * 5 * STAMP_WAVES * STAMP_SLOTS;
@@ -1939,11 +2211,13 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   const bool merge = !c->sk && c->K >= MMSBM_LDS_BIG && !(mg && mg[0] == '0');
   // stream-0 partial rows per S partial at large K (each S partial is K^3 words the update sums);
   // MMSBM_SP_ROWS=n overrides it (measurement)
-  int sp_rows = c->K <= 12 ? 16 : 4 * c->K;
+  // gm_kernel (round 5): 128 rows (two 64-row tiles) per part and no cap on the parts
+  int sp_rows = c->K <= 12 ? 16 : c->gm ? 128 : 4 * c->K;
   if (const char* e = getenv("MMSBM_SP_ROWS")) sp_rows = std::max(4, atoi(e));
+  const int sp_cap = (!c->sk && c->gm) ? (1 << 30) : 256;
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
                            c->gcap, sp_rows, c->sk, 1024, c->sk_fused,
-                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge);
+                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge, sp_cap);
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
   sd.unit_target = c->sk_fused ? units_a : 0;
@@ -2021,6 +2295,7 @@ int mmsbm_set_workspace(mmsbm_ctx* c, void* ws, int64_t bytes) {
   c->partL = (double*)(c->ws + L.partL);
   c->nth_tmp = (double*)(c->ws + L.nth);
   c->S_tmp = (double*)(c->ws + L.S);
+  c->xrows = c->sk ? nullptr : (double*)(c->ws + L.xrows);
   // small-K: the c vector's last slot (stream-1/2 padding rows read it) and the S partials stay
   // zero; large-K: Y and the S partials start zeroed (every word read is written each iteration)
   HIP_TRY(hipMemset(c->ws + L.cbuf, 0, L.prows - L.cbuf));

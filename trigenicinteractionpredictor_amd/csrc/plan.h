@@ -256,11 +256,11 @@ inline void make_slots(Plan& pl) {
 // Builds the plan.  units_a / units_b: the number of units to aim for in stream 0 and in streams
 // 1 + 2 together (about 8 waves per CU); gcap: most distinct genes per stream-0 workgroup (its
 // V table lives in LDS); sp_rows: stream-0 partial rows per S-partial workgroup (each writes a
-// K^3 partial, so large K wants more rows per partial).
+// K^3 partial, so large K wants more rows per partial), at most sp_cap of them per rating.
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
                   int wg_target = 1024, bool fill = false, int gu = GU, int rho_pct = 85,
-                  bool yent = false, bool balance = true, bool merge = false) {
+                  bool yent = false, bool balance = true, bool merge = false, int sp_cap = 256) {
   Plan pl;
   pl.merge = merge && balance && !small && em;
   pl.gu = std::max(1, std::min(gu, GU));
@@ -592,7 +592,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       const int q1 = pl.prow_ptr[(size_t)r * (P + 1) + P];
       pl.sp_lo[r] = pl.n_sp;
       const int n = q1 - q0;
-      const int parts = n <= 0 ? 0 : std::min(256, std::max(1, n / std::max(sp_rows, 1)));
+      const int parts = n <= 0 ? 0 : std::min(sp_cap, std::max(1, (n + sp_rows - 1) / std::max(sp_rows, 1)));
       for (int k = 0; k < parts; ++k) {
         pl.sp_desc.push_back(r);
         pl.sp_desc.push_back(q0 + (int)((long long)n * k / parts));
