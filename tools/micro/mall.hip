@@ -29,6 +29,16 @@ __global__ __launch_bounds__(256) void write_seq(d2* __restrict__ y, long long n
   y[g] = d2{v, v + 1.0};
 }
 
+// 16 lanes per 256-B entry: entry e read from slot perm[e] (a gather of whole entries)
+__global__ __launch_bounds__(256) void read_gather(const d2* __restrict__ y, const int* __restrict__ perm, long long n_ent,
+                                                   double* __restrict__ out) {
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long e = g >> 4;
+  if (e >= n_ent) return;
+  const d2 a = y[(long long)perm[e] * 16 + (threadIdx.x & 15)];
+  if (a.x == -1.2345) out[0] = a.y;
+}
+
 __global__ __launch_bounds__(256) void read_seq(const d2* __restrict__ y, long long n_ent, double* __restrict__ out) {
   const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
   if ((g >> 4) >= n_ent) return;
@@ -69,7 +79,8 @@ int main() {
     return 1;
   }
   std::vector<int> h(maxb / 256);
-  printf("%10s %12s %12s %12s %14s %14s\n", "MB", "wr_seq GB/s", "wr_scat GB/s", "rd GB/s", "wr+rd GB/s", "rt vs 5GB");
+  printf("%10s %12s %12s %12s %12s %14s %14s\n", "MB", "wr_seq GB/s", "wr_scat GB/s", "rd GB/s", "rd_gath GB/s",
+         "scat+rd GB/s", "seq+gath GB/s");
   double base_rt = 0;
   std::vector<double> rts;
   for (long long S : sizes) {
@@ -82,13 +93,18 @@ int main() {
     const float tw = med_us([&] { write_seq<<<nb, 256>>>(y, n, 1.0); }, 9);
     const float ts = med_us([&] { write_scatter<<<nb, 256>>>(y, perm, n, 1.0); }, 9);
     const float tr = med_us([&] { read_seq<<<nb, 256>>>(y, n, out); }, 9);
+    const float tg = med_us([&] { read_gather<<<nb, 256>>>(y, perm, n, out); }, 9);
     const float trt = med_us([&] {
       write_scatter<<<nb, 256>>>(y, perm, n, 2.0);
       read_seq<<<nb, 256>>>(y, n, out);
     }, 9);
+    const float trt2 = med_us([&] {
+      write_seq<<<nb, 256>>>(y, n, 2.0);
+      read_gather<<<nb, 256>>>(y, perm, n, out);
+    }, 9);
     const double gb = S / 1e9;
-    printf("%10lld %12.0f %12.0f %12.0f %14.0f\n", S / MB, gb / (tw * 1e-6), gb / (ts * 1e-6), gb / (tr * 1e-6),
-           2 * gb / (trt * 1e-6));
+    printf("%10lld %12.0f %12.0f %12.0f %12.0f %14.0f %14.0f\n", S / MB, gb / (tw * 1e-6), gb / (ts * 1e-6),
+           gb / (tr * 1e-6), gb / (tg * 1e-6), 2 * gb / (trt * 1e-6), 2 * gb / (trt2 * 1e-6));
     rts.push_back(2 * gb / (trt * 1e-6));
   }
   // ring of two 96 MB regions against one 5 GB stream, same bytes: 52 write+read round trips

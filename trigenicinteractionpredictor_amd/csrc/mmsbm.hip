@@ -1327,7 +1327,8 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
     SpRange spr, int P, int R, int n_sp, int n_th_wg, double eps, double* __restrict__ nth_out,
     double* __restrict__ S_out, const double* __restrict__ nth_add, const double* __restrict__ q_part,
     double* __restrict__ q_out, int n_qwg, const double* __restrict__ xrow, const int* __restrict__ prow_ptr,
-    long long n_prows, long long xgs) {
+    long long n_prows, long long xgs, const double* __restrict__ ybuf, const int* __restrict__ yptr,
+    long long n_y) {
   constexpr int K2 = K * K, K3 = K * K * K;
   constexpr int NCW = (K3 + 63) / 64, NPART = UPD_NT / 64;
   __shared__ double red[MAX_R * NPART * 64];
@@ -1348,7 +1349,23 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
           for (int h = 1; h < GM<K>::CS; ++h) x += xb[h * xgs + (size_t)q * K];
           X += x;
         }
-      X += ysum[o];
+      if (ybuf) {  // the gene's Y entries, summed here (no ysum launch): entry order, 8 loads in flight
+        constexpr int YU = FT<K>::YU, YS = y_stride(K);
+        const double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * YS + a;
+        const int e0 = yptr[g], e1 = yptr[g + 1];
+        double Y = 0.0;
+        for (int e = e0; e < e1; e += YU) {
+          double v[YU];
+#pragma unroll
+          for (int u = 0; u < YU; ++u) v[u] = yb[(size_t)(e + u < e1 ? e + u : e) * YS];
+#pragma unroll
+          for (int u = 0; u < YU; ++u)
+            if (e + u < e1) Y += v[u];
+        }
+        X += Y;
+      } else {
+        X += ysum[o];
+      }
     } else {
       X = x0[o] + ysum[o];
     }
@@ -1641,6 +1658,7 @@ struct mmsbm_ctx {
   bool gsplit = true;
   // large-K M-step contractions in gm_kernel (round 5); MMSBM_GM=0: round 4's gene kernel (measurement)
   bool gm = MMSBM_GM != 0;
+  bool yupd = true;              // gm path: Y sums inside upd_kernel (MMSBM_YUPD=0: own launch)
   double* xrows = nullptr;       // gm_kernel's X rows [B][n_prows][K]
   hipStream_t ys = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -1763,9 +1781,11 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
           theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, h.n_prows,
           std::max(h.n_sp, 1), (long long)c->B * h.n_prows * K);
       HIP_TRY(hipGetLastError());
-      const long long nyb = ((long long)c->P * K + 255) / 256;
-      ysum_kernel<K><<<dim3((unsigned)nyb, nb_of(c)), 256, 0, s>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
-      HIP_TRY(hipGetLastError());
+      if (!c->yupd) {  // MMSBM_YUPD=0 (measurement): the Y sums as a launch of their own
+        const long long nyb = ((long long)c->P * K + 255) / 256;
+        ysum_kernel<K><<<dim3((unsigned)nyb, nb_of(c)), 256, 0, s>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
+        HIP_TRY(hipGetLastError());
+      }
       return MMSBM_OK;
     }
     // two launches from K = 24 (K=30 gene 1,778 -> 1,745 us, profiles/r04w_gsplit_ab.txt); at
@@ -1828,15 +1848,18 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   // joint model: the q cells (qr M-step from the pair launch's S2 partials), theta update only
   const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
   const double* xr = c->gm ? c->xrows : nullptr;  // gm_kernel's X rows, or gene_kernel's x0
+  // gm path: the theta workgroups sum each gene's Y entries themselves (round 5)
+  const double* yb = (c->gm && c->yupd) ? c->cbuf : nullptr;
   if (sums)
     upd_kernel<K, true><<<dim3(nthw + ncw, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
-        nth, S, c->nth_add, nullptr, nullptr, 0, xr, sd.prow_ptr, h.n_prows, (long long)c->B * h.n_prows * K);
+        nth, S, c->nth_add, nullptr, nullptr, 0, xr, sd.prow_ptr, h.n_prows, (long long)c->B * h.n_prows * K,
+        yb, sd.yptr, h.n_y);
   else
     upd_kernel<K, false><<<dim3(nthw + ncw + nqc, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
         nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg, xr, sd.prow_ptr, h.n_prows,
-        (long long)c->B * h.n_prows * K);
+        (long long)c->B * h.n_prows * K, yb, sd.yptr, h.n_y);
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -2064,6 +2087,7 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   if (const char* ysp = getenv("MMSBM_YSPLIT")) c->ysplit = ysp[0] != '0';
   if (const char* gsp = getenv("MMSBM_GSPLIT")) c->gsplit = gsp[0] != '0';
   if (const char* gme = getenv("MMSBM_GM")) c->gm = gme[0] != '0';
+  if (const char* yu = getenv("MMSBM_YUPD")) c->yupd = yu[0] != '0';
   if (MMSBM_STAMP && getenv("MMSBM_STAMP")) {
     DeviceGuard g(device);
     const size_t bytes = sizeof(unsigned long long) * 5 * STAMP_WAVES * STAMP_SLOTS;
