@@ -14,8 +14,8 @@
 #                                  rocprofv3 kernel-trace stats, the PMC passes (one counter
 #                                  group per pass) and the build-stamped traffic record NAME.pmc.json
 #   ab NAME "bench args" VARIANT...
-#                                  A/B on one box, each VARIANT a library path ("-" = in-tree) or
-#                                  "env:VAR=v,VAR2=v" run against the in-tree library
+#                                  A/B on one box, each VARIANT a library path ("-" = in-tree),
+#                                  "env:VAR=v,VAR2=v" (in-tree library) or "LIB+env:VAR=v"
 #   py NAME SCRIPT [args]          a tools/ script (GPU measurement aid) -> NAME.txt
 #   stamp NAME LIB [bench args]    per-wave phase stamps of a stamp build (tools/build_variant.py
 #                                  LIB -DMMSBM_STAMP=1), analysed by tools/stamp_analyze.py
@@ -90,10 +90,11 @@ PY
     local i=0
     for v in "$@"; do
       i=$((i+1))
-      local envs=""
+      local envs="" lib="$v"
       unset MMSBM_LIB
-      if [ "${v#env:}" != "$v" ]; then envs=$(echo "${v#env:}" | tr ',' ' ');
-      elif [ "$v" != "-" ]; then export MMSBM_LIB=$R/$v; fi
+      if [ "${v#*+env:}" != "$v" ]; then lib="${v%%+env:*}"; envs=$(echo "${v#*+env:}" | tr ',' ' ');
+      elif [ "${v#env:}" != "$v" ]; then lib="-"; envs=$(echo "${v#env:}" | tr ',' ' '); fi
+      if [ "$lib" != "-" ]; then export MMSBM_LIB=$R/$lib; fi
       timeout -k 10 500 env $envs python -u bench.py --no-cpu-baseline $args > "$OUT/${name}_$i.json" 2> "$OUT/${name}_$i.err" || { echo "ab $name variant $v failed"; tail -10 "$OUT/${name}_$i.err"; return 1; }
       echo -n "[$v] "; summ "$OUT/${name}_$i.json"
     done
