@@ -241,29 +241,11 @@ int main() {
   const bool balance = !getenv("PLAN_NO_BALANCE");
   // PLAN_MERGE=1: one partial row per (workgroup, gene) (the K >= 25 pass kernel merges its waves' parts)
   const bool merge = getenv("PLAN_MERGE") != nullptr;
-  // PLAN_BLK=4: stream-0 runs padded to 16-row blocks, units split at blocks (pass16_kernel, K >= 25)
-  const int blk = getenv("PLAN_BLK") ? atoi(getenv("PLAN_BLK")) : 1;
   const int gu = (gcap == 0 || gcap == -2) ? 4 : 8;
   const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill, gu,
                                 85, yent)
                         : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows, false, 1024,
-                                false, GU, 85, false, balance, merge, 256, blk);
-  if (!small && blk > 1 && balance) {
-    // blocks: unit / workgroup boundaries at multiples of blk chunks; every block of blk chunks one
-    // pivot gene (stream 0, pivot = slot 0), one partial row and one V slot
-    if (pl.blk != blk) return fail("plan blk", pl.blk, blk);
-    for (size_t u = 0; u < pl.wg_units.size(); ++u)
-      if (pl.wg_units[u] % blk) return fail("unit boundary inside a block", (long long)u, pl.wg_units[u]);
-    const long long nch0 = pl.n_rows0 / CH;
-    if (nch0 % blk) return fail("stream-0 chunks", nch0);
-    for (long long c0 = 0; c0 < nch0; c0 += blk)
-      for (long long c = c0; c < c0 + blk; ++c) {
-        if (pl.chunk_prow[c] != pl.chunk_prow[c0] || pl.chunk_vslot[c] != pl.chunk_vslot[c0])
-          return fail("block row / slot", c0, c);
-        for (int i = 0; i < CH; ++i)
-          if (pl.rows[c * CH + i].x != pl.rows[c0 * CH].x) return fail("block pivot", c0, c);
-      }
-  }
+                                false, GU, 85, false, balance, merge);
   if (fill) {  // every unit but the last of its (stream, rating) section is full: LCAP_SK chunks or GU stretches
     for (long long u = 0; u + 1 < pl.n_units; ++u) {
       const int* d = &pl.udesc[(size_t)u * UD];
@@ -329,10 +311,8 @@ int main() {
       umax = std::max(umax, c1 - c0);
       for (int c = c0; c < c1; ++c) covered[c]++;
     }
-    // balanced packing: a workgroup's NW units differ by at most one chunk (one block of blk chunks
-    // for stream 0 when its units split at blocks)
-    const int tol = (s == 0 && blk > 1) ? blk : 1;
-    if (balance && umax - umin > tol) return fail("unbalanced units", w, umax - umin);
+    // balanced packing: a workgroup's NW units differ by at most one chunk
+    if (balance && umax - umin > 1) return fail("unbalanced units", w, umax - umin);
     if (s == 0) {
       const int g0 = pl.wg_gene[w], g1 = pl.wg_gene[w + 1];
       if (g1 - g0 > gcap || g1 - g0 > pl.gmax) return fail("gene cap", w, g1 - g0);

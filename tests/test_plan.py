@@ -113,16 +113,3 @@ def test_balanced_plan_fewer_workgroups(plan_check):
     bal = _check(plan_check, 500, 40000, (64, 64), 5, 120, 0.0)
     old = _check(plan_check, 500, 40000, (64, 64), 5, 120, 0.0, env={"PLAN_NO_BALANCE": "1"})
     assert int(bal[3]) < int(old[3])
-
-
-# 16-row blocks (pass16_kernel, K >= 25: PLAN_BLK=4) with merged rows: every invariant above plus
-# block-aligned units and one pivot gene, partial row and V slot per block
-@pytest.mark.parametrize("P,E,units,gcap,sp_rows,hub", [
-    (500, 40000, (64, 64), 10, 128, 0.0),
-    (300, 5000, (1536, 3072), 10, 128, 30.0),
-    (40, 600, (1, 1), 10, 16, 0.0),
-    (3000, 4000, (1536, 3072), 10, 128, 0.0),    # one or two observations per gene: mostly padding
-])
-def test_plan_invariants_blocks(plan_check, P, E, units, gcap, sp_rows, hub):
-    _check(plan_check, P, E, units, gcap, sp_rows, hub, env={"PLAN_BLK": "4", "PLAN_MERGE": "1"})
-    _check(plan_check, P, E, units, gcap, sp_rows, hub, env={"PLAN_BLK": "4"})

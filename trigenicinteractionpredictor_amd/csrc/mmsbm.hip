@@ -103,14 +103,6 @@ constexpr int lds_target(int K) { return K >= MMSBM_LDS_BIG ? 150 * 1024 : K <= 
 #define MMSBM_YALIGN 4
 #endif
 constexpr int y_stride(int K) { return (K + MMSBM_YALIGN - 1) / MMSBM_YALIGN * MMSBM_YALIGN; }
-// Entries per sample of the large-K Y buffer: the plan's n_y, then YPAD spare entries that padding
-// rows (and pad words) write instead of the real ones, spread so no two waves share one line
-// (a single dummy entry made every padding store of the chip hit one L2 line, and a branch around
-// the stores made the compiler's vmcnt waits drain the previous block's Y stores)
-constexpr int YPAD = 4096;
-#ifndef MMSBM_YSPARE
-#define MMSBM_YSPARE 1
-#endif
 
 // Pass-kernel occupancy hint: 1 leaves the compiler free (K = 25-32 take 132-134 VGPRs, so one
 // 8-wave workgroup per CU although the LDS would fit two); 4 caps it at 128 VGPRs (4 waves per
@@ -175,8 +167,7 @@ struct KT {
   static_assert(64 * KP * 8 <= IMG_BYTES, "S partial staging over the pass B LDS");
 };
 
-int gmax_for(int K);    // host view of KT<K>::GMAX (table below)
-int gmax16_for(int K);  // host view of P16<K>::GMAX
+int gmax_for(int K);  // host view of KT<K>::GMAX (table below)
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
@@ -525,7 +516,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   double* __restrict__ pb = prows + (size_t)b * n_prows * T::K2;
   constexpr int YS = y_stride(K);
   static_assert(YS <= 16 * T::NBG, "Y stride within the Z / Z' lanes");
-  double* __restrict__ yb = ybuf + (size_t)b * (n_y + YPAD) * YS;
+  double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * YS;
   // staged pieces of one chunk: piece pc = 64 t + lane is SW doubles of row8 = pc / (KP / SW)
   // (rows 0-3: th_u = th_j of obs 0-3, rows 4-7: th_v = th_k), columns SW (pc % (KP / SW)) ..
   typedef double d2v __attribute__((ext_vector_type(2)));  // a native vector: SROA-friendly
@@ -620,12 +611,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
           // ---- the j- and k-slot sums of this observation (:1009-1011): Y[entry j][b] = c Z[b]
           // and Y[entry k][h] = c Z'[h], Z'[h] = sum_b th_j[b] V[b][h]; 16 lanes of row hi write
           // 16 consecutive words of observation hi's entry
-          int e1 = __shfl(rq, 18 + 2 * hi, 64), e2 = __shfl(rq, 19 + 2 * hi, 64);
-          if (MMSBM_YSPARE && e1 >= n_y) {  // a padding row: this wave's spare entries (YPAD), not one shared line
-            const int sp = (int)(n_y + ((wave_id * 8 + 2 * hi) & (YPAD - 2)));
-            e1 = sp;
-            e2 = sp + 1;
-          }
+          const int e1 = __shfl(rq, 18 + 2 * hi, 64), e2 = __shfl(rq, 19 + 2 * hi, 64);
           double au[NG];  // th_u[obs lo][4 bs + hi]: the A operand of Z'
 #pragma unroll
           for (int bs = 0; bs < NG; ++bs) au[bs] = I[lo * TR + 4 * bs + hi];
@@ -768,352 +754,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   }
   st_.mark(3);
   st_.flush(MODE == PASS_A ? 0 : 4, wave_id, lane);
-}
-
-// ------------------------------------------------------------------------------------------
-// pass16_kernel (round 5): PASS_A from K = MMSBM_A16 (default 25) in BLOCKS of 16 observations of one
-// pivot gene (Plan blk = 4: stream-0 runs padded to 16 rows, units split at blocks), every
-// per-observation contraction on v_mfma_f64_16x16x4f64 with the block's 16 observations as the
-// MFMA rows (src/TrigenicInteractionPredictor.py:996-1012):
-//   Z[o][b]  = sum_h th_k(o)[h] V_g[b][h]     2 b tiles x 8 k-steps
-//   Z'[o][h] = sum_b th_j(o)[b] V_g[b][h]     2 h tiles x 8 k-steps
-//   d = eps + th_j . Z (DPP row sums), c = n / d, Y entries c Z (gene j), c Z' (gene k),
-//   M += c th_j (x) th_k (k = the observations: 4 steps x 4 tiles)
-// The A operands' k order (h = 8 t + s for lane group t = lane / 16 and step s) lets every lane
-// gather 8 contiguous doubles of its observation's theta row straight into registers; the copies in
-// the D layout (observation t + 4 i, column 16 tile + lane % 16) that d and M need go through a
-// per-wave LDS image (16 x 32 per matrix, column XOR (o & 1) 16).  V tables are stored with column
-// h ^ vsw(b) (bits 0-2 <- b bits 0-2, bit 4 <- b bit 3), so the Z operand (16 rows x 2 columns) and
-// the Z' operand (2 rows x 16 columns) are both conflict-free ds_read_b64.  Per 16 observations: 48
-// MFMA16 and 48 LDS reads, against 128 MFMA4 + 16 MFMA16 and ~216 LDS reads for the four
-// 4-observation chunks of pass_kernel; one dependent chain per block instead of per chunk.
-// Prologue (V tables), merged partial rows and the Y-entry layout are pass_kernel's.
-// ------------------------------------------------------------------------------------------
-#ifndef MMSBM_A16
-#define MMSBM_A16 0
-#endif
-template <int K>
-struct P16 {
-  static constexpr int NG = (K + 3) / 4, KP = 4 * NG;    // 4-wide tiles (the V prologue's)
-  static constexpr int VS = 32;                           // V row stride; 32 rows (b >= K zero)
-  static constexpr int VDBL = 32 * VS;
-  static constexpr int TGR = KP + 1;                      // theta rows of the V genes
-  static constexpr int tg_dbl(int g) { return (g * TGR + 1) & ~1; }
-  static constexpr int IMGW = 2 * 16 * 32;                // per wave: th_j and th_k images
-  static constexpr int IMG_BYTES = NW * IMGW * 8;
-  static constexpr int GMAX_RAW = (150 * 1024 - IMG_BYTES - 64 - 8) / ((VDBL + TGR) * 8);
-  static constexpr int GMAX = GMAX_RAW > 64 ? 64 : (GMAX_RAW < 4 ? 4 : GMAX_RAW);
-  static constexpr int LDS = GMAX * VDBL * 8 + tg_dbl(GMAX) * 8 + IMG_BYTES + 64;
-  static constexpr int SW = K % 2 == 0 ? 2 : 1;           // gather width (rows 16-B aligned)
-  static_assert(K > 16 && K <= 32, "pass16: two 16-wide tiles");
-  static_assert(LDS <= 160 * 1024, "pass16 LDS over budget");
-};
-
-__device__ __forceinline__ int vsw16(int b) { return (b & 7) | ((b & 8) << 1); }
-
-template <int K>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) void pass16_kernel(
-    const int4* __restrict__ rows, const int* __restrict__ chunk_prow, const int* __restrict__ chunk_vslot,
-    const int* __restrict__ row_y, const int* __restrict__ wg_units, const int* __restrict__ wg_code,
-    const int* __restrict__ wg_gene, const int* __restrict__ vgenes, const double* __restrict__ theta,
-    const double* __restrict__ pr, double* __restrict__ ybuf, double* __restrict__ prows, int P, int R,
-    long long n_y, long long n_prows, int n_wg, double eps, int gcap, int merge) {
-  using T = P16<K>;
-  constexpr int VS = T::VS, SW = T::SW;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int t = lane >> 4, j = lane & 15;                           // (block loop lane map)
-  const int w = blockIdx.x, b = blockIdx.y;
-  const double* __restrict__ th = theta + (size_t)b * P * K;
-  Stamp st_{};
-  st_.mark(0);
-  const int r = wg_code[w] & 15;
-  const double* __restrict__ p = pr + ((size_t)b * R + r) * K * K * K;
-  double* Vt = smem;
-  double* imj = smem + gcap * T::VDBL + T::tg_dbl(gcap) + wv * T::IMGW;  // [16][32] th_j
-  double* imk = imj + 16 * 32;                                            // [16][32] th_k
-  // this wave's blocks (chunks / 4)
-  const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
-  const int q0 = c0 >> 2, q1 = c1 >> 2;
-  const bool any = q0 < q1;
-  bool first_cont = false, last_cont = false;
-  if (merge && any) {
-    const int wc0 = wg_units[w * (NW + 1)], wc1 = wg_units[w * (NW + 1) + NW];
-    first_cont = c0 > wc0 && __builtin_amdgcn_readfirstlane(chunk_prow[c0 - 1]) ==
-                                 __builtin_amdgcn_readfirstlane(chunk_prow[c0]);
-    last_cont = c1 < wc1 && __builtin_amdgcn_readfirstlane(chunk_prow[c1]) ==
-                                __builtin_amdgcn_readfirstlane(chunk_prow[c1 - 1]);
-  }
-  // records of block q, observation j of this lane: (i, j, k, w) and its two Y entries
-  auto clampq = [&](int q) { return q < q1 ? q : q1 - 1; };
-  auto ld_rec = [&](int q, int4& rc, int2& ey) {
-    const long long row = 16LL * clampq(q) + j;
-    rc = rows[row];
-    ey = *reinterpret_cast<const int2*>(row_y + 2 * row);
-  };
-  int4 rcA, rcB, rcC;
-  int2 eyA, eyB, eyC;
-  if (any) {
-    ld_rec(q0, rcA, eyA);
-    ld_rec(q0 + 1, rcB, eyB);
-  }
-
-  {
-    // ---- V_g[b][h] = sum_a th_g[a] p_r[a][b][h] for the workgroup's pivot genes, one GEMM on
-    // v_mfma_f64_16x16x4: rows = the genes (<= GMAX <= 16), k = a (8 steps), columns = 16 h of one
-    // b (tile (b, ht), 2 K tiles over the 8 waves).  Lane (t, j) holds th_{gene j}[4 s + t] for the 8
-    // steps; its B operand is p_r[4 s + t][b][16 ht + j] (16 lanes read 128 contiguous bytes, L2),
-    // the next tile's 8 loads in flight during this tile's MFMAs.  Stored at column h ^ vsw16(b);
-    // rows b >= K zero, columns h >= K zero through the zeroed operands.
-    const int ng = wg_gene[w + 1] - wg_gene[w];
-    const int* __restrict__ vgw = vgenes + (size_t)w * gcap;
-    static_assert(T::GMAX <= 16, "pass16 prologue: one 16-row gene tile");
-    double ta[8];
-    {
-      const int g = vgw[j < gcap ? j : 0];
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8) {
-        const int a = 4 * s8 + t;
-        const double v = th[(size_t)g * K + (a < K ? a : 0)];
-        ta[s8] = (j < ng && a < K) ? v : 0.0;
-      }
-    }
-    {
-      constexpr int ZR = (32 - K) * VS;
-      for (int idx = tid; idx < ng * ZR; idx += NT) Vt[(idx / ZR) * T::VDBL + K * VS + idx % ZR] = 0.0;
-    }
-    st_.mark(6);
-    constexpr int NTILE = 2 * K;
-    auto v_load = [&](int tile, double (&pv)[8]) {
-      const int bb = tile >> 1, h = 16 * (tile & 1) + j;
-      const bool tv = tile < NTILE && h < K;
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8) {
-        const int a = 4 * s8 + t;
-        const bool ok = tv && a < K;
-        const double v = p[ok ? ((size_t)a * K + bb) * K + h : 0];
-        pv[s8] = ok ? v : 0.0;
-      }
-    };
-    auto v_tile = [&](int tile, const double (&pv)[8]) {
-      d4v acc = d4v{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8) acc = mfma16(ta[s8], pv[s8], acc);
-      const int bb = tile >> 1, h = 16 * (tile & 1) + j;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int go = t + 4 * e;
-        if (go < ng) Vt[go * T::VDBL + bb * VS + (h ^ vsw16(bb))] = acc[e];
-      }
-    };
-    double pA[8], pB[8];
-    v_load(wv, pA);
-    for (int tile = wv; tile < NTILE; tile += 2 * NW) {
-      v_load(tile + NW, pB);
-      v_tile(tile, pA);
-      v_load(tile + 2 * NW, pA);
-      if (tile + NW < NTILE) v_tile(tile + NW, pB);
-    }
-    __syncthreads();
-  }
-  st_.mark(1);
-
-  double* __restrict__ pb = prows + (size_t)b * n_prows * K * K;
-  constexpr int YS = y_stride(K);
-  double* __restrict__ yb = ybuf + (size_t)b * (n_y + YPAD) * YS;
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  using SV = typename std::conditional<SW == 2, d2v, double>::type;
-  constexpr int NPIECE = 8 / SW;
-  // A-layout gather: columns 8 t .. 8 t + 7 of observation j's th_j (gene .y) and th_k (.z) rows;
-  // columns >= K load a clamped address and are zeroed
-  auto gather = [&](const int4& rc, double (&aj)[8], double (&ak)[8]) {
-#pragma unroll
-    for (int u = 0; u < NPIECE; ++u) {
-      const int col = 8 * t + SW * u;
-      const int cc = col + SW <= K ? col : K - SW;
-      const SV vj = *reinterpret_cast<const SV*>(th + (size_t)rc.y * K + cc);
-      const SV vk = *reinterpret_cast<const SV*>(th + (size_t)rc.z * K + cc);
-#pragma unroll
-      for (int e = 0; e < SW; ++e) {
-        const bool ok = col + e < K;
-        double xj, xk;
-        if constexpr (SW == 2) { xj = vj[e]; xk = vk[e]; } else { xj = vj; xk = vk; }
-        aj[SW * u + e] = ok ? xj : 0.0;
-        ak[SW * u + e] = ok ? xk : 0.0;
-      }
-    }
-  };
-  constexpr int NX16 = 2;
-  d4v m16[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) m16[u] = d4v{0.0, 0.0, 0.0, 0.0};
-  d4v mc[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) mc[u] = d4v{0.0, 0.0, 0.0, 0.0};
-  bool first_st = true, kept = false;
-  const int zsw = (8 * t) ^ ((j & 8) << 1), jm = j & 7;  // Z operand column: zsw | (s ^ jm)
-  const int ywave = (int)((((long long)b * gridDim.x + w) * NW + wv) * 32);  // spare-entry spread
-  const int isw = (t & 1) << 4;                           // image column swizzle of rows t + 4 i
-  double aj[8], ak[8], nj[8], nk[8];
-  if (any) gather(rcA, aj, ak);
-  for (int q = q0; q < q1; ++q) {
-    // prefetch: records of q + 2, theta of q + 1
-    ld_rec(q + 2, rcC, eyC);
-    gather(rcB, nj, nk);
-    // this block's A-layout rows into the image (the D-layout reads below)
-    {
-      const int rs = (j & 1) << 4;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int col = (8 * t + 2 * u) ^ rs;
-        *reinterpret_cast<d2v*>(imj + j * 32 + col) = d2v{aj[2 * u], aj[2 * u + 1]};
-        *reinterpret_cast<d2v*>(imk + j * 32 + col) = d2v{ak[2 * u], ak[2 * u + 1]};
-      }
-    }
-    wave_lds_sync();
-    const int c = 4 * q;
-    const int pr0 = __builtin_amdgcn_readfirstlane(chunk_prow[c]);
-    const int pr1 = __builtin_amdgcn_readfirstlane(chunk_prow[c + 4 < c1 ? c + 4 : c]);
-    const double* __restrict__ V = Vt + __builtin_amdgcn_readfirstlane(chunk_vslot[c]) * T::VDBL;
-    // ---- Z (D: obs t + 4 i, b = 16 bt + j) and Z' (h = 16 ht + j)
-    d4v z0 = d4v{0.0, 0.0, 0.0, 0.0}, z1 = z0, y0 = z0, y1 = z0;
-#pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8) {
-      const int zc = zsw | (s8 ^ jm);
-      z0 = mfma16(ak[s8], V[j * VS + zc], z0);
-      z1 = mfma16(ak[s8], V[(16 + j) * VS + zc], z1);
-      const int br = 8 * t + s8;  // Z' operand: V row br, columns (16 ht + j) ^ vsw16(br)
-      const int yc = ((t & 1) << 4) | (j ^ s8);
-      y0 = mfma16(aj[s8], V[br * VS + yc], y0);
-      y1 = mfma16(aj[s8], V[br * VS + (yc ^ 16)], y1);
-    }
-    // ---- D-layout theta: dj[i][x tile], dk[i][y tile] of observation t + 4 i
-    double dj[4][2], dk[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int xt = 0; xt < 2; ++xt) {
-        const int col = ((16 * xt) ^ isw) + j;
-        dj[i][xt] = imj[(t + 4 * i) * 32 + col];
-        dk[i][xt] = imk[(t + 4 * i) * 32 + col];
-      }
-    // ---- d, c of observations t + 4 i (all 16 lanes of group t agree)
-    double cv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const double dp = fma(dj[i][1], z1[i], dj[i][0] * z0[i]);
-      const double dd = row16_sum(dp) + eps;
-      const int nw = __shfl(rcA.w, t + 4 * i, 64);
-      cv[i] = (double)nw / dd;
-    }
-    // ---- Y entries (:1009-1011): c Z -> entry of slot 1 (gene j), c Z' -> slot 2 (gene k)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      // every lane stores every time (a branch here costs the vmcnt waits, see YPAD): a padding row,
-      // or a pad word past YS, goes to this wave's spare entries
-      const int e1 = __shfl(eyA.x, t + 4 * i, 64), e2 = __shfl(eyA.y, t + 4 * i, 64);
-      const size_t spare = ((size_t)n_y + ((ywave + 2 * (t + 4 * i)) & (YPAD - 2))) * YS;
-      const size_t a1 = e1 < n_y ? (size_t)e1 * YS : spare, a2 = e2 < n_y ? (size_t)e2 * YS : spare + YS;
-      yb[a1 + j] = cv[i] * z0[i];
-      yb[a2 + j] = cv[i] * y0[i];
-      const bool hv = 16 + j < YS;
-      yb[hv ? a1 + 16 + j : spare + j] = cv[i] * z1[i];
-      yb[hv ? a2 + 16 + j : spare + YS + j] = cv[i] * y1[i];
-    }
-    // ---- M += c th_j (x) th_k: k = observation t + 4 i
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int xt = 0; xt < 2; ++xt)
-#pragma unroll
-        for (int yt = 0; yt < 2; ++yt)
-          m16[xt * 2 + yt] = mfma16(dj[i][xt], cv[i] * dk[i][yt], m16[xt * 2 + yt]);
-    if (q + 1 >= q1 || pr1 != pr0) {  // end of this gene stretch: its partial row
-      const bool to_mc = first_st && first_cont;
-      const bool keep = !to_mc && q + 1 >= q1 && last_cont;
-      first_st = false;
-      kept = keep;
-      if (to_mc) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          mc[u] = m16[u];
-          m16[u] = d4v{0.0, 0.0, 0.0, 0.0};
-        }
-      } else if (!keep) {
-        double* __restrict__ out = pb + (size_t)pr0 * K * K;
-#pragma unroll
-        for (int tx = 0; tx < NX16; ++tx)
-#pragma unroll
-          for (int ty = 0; ty < NX16; ++ty)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int x = 16 * tx + t + 4 * i, y = 16 * ty + j;
-              if (x < K && y < K) st_wt(out + x * K + y, m16[tx * NX16 + ty][i]);
-              m16[tx * NX16 + ty][i] = 0.0;
-            }
-      }
-    }
-    wave_lds_sync();  // the image is rewritten by the next block
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      aj[e] = nj[e];
-      ak[e] = nk[e];
-    }
-    rcA = rcB;
-    eyA = eyB;
-    rcB = rcC;
-    eyB = eyC;
-  }
-  st_.mark(2);
-  if (merge) {  // (workgroup-uniform) the V tables and images are dead: NW slots of K^2 words
-    static_assert((4 * T::VDBL + T::tg_dbl(4)) * 8 + T::IMG_BYTES >= NW * K * K * 8, "merge slots");
-    __syncthreads();
-    if (first_cont) {
-#pragma unroll
-      for (int tx = 0; tx < NX16; ++tx)
-#pragma unroll
-        for (int ty = 0; ty < NX16; ++ty)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int x = 16 * tx + t + 4 * i, y = 16 * ty + j;
-            if (x < K && y < K) smem[wv * K * K + x * K + y] = mc[tx * NX16 + ty][i];
-          }
-    }
-    __syncthreads();
-    if (kept) {
-      const int mypr = __builtin_amdgcn_readfirstlane(chunk_prow[c1 - 1]);
-      for (int nx = wv + 1; nx < NW; ++nx) {  // the continuing waves, in order
-        const int n0 = wg_units[w * (NW + 1) + nx], n1 = wg_units[w * (NW + 1) + nx + 1];
-        if (n0 == n1) continue;
-        if (__builtin_amdgcn_readfirstlane(chunk_prow[n0]) != mypr) break;
-#pragma unroll
-        for (int tx = 0; tx < NX16; ++tx)
-#pragma unroll
-          for (int ty = 0; ty < NX16; ++ty)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int x = 16 * tx + t + 4 * i, y = 16 * ty + j;
-              if (x < K && y < K) m16[tx * NX16 + ty][i] += smem[nx * K * K + x * K + y];
-            }
-        if (__builtin_amdgcn_readfirstlane(chunk_prow[n1 - 1]) != mypr) break;
-      }
-      double* __restrict__ out = pb + (size_t)mypr * K * K;
-#pragma unroll
-      for (int tx = 0; tx < NX16; ++tx)
-#pragma unroll
-        for (int ty = 0; ty < NX16; ++ty)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int x = 16 * tx + t + 4 * i, y = 16 * ty + j;
-            if (x < K && y < K) st_wt(out + x * K + y, m16[tx * NX16 + ty][i]);
-          }
-    }
-  }
-  st_.t[5] = (unsigned long long)(c1 - c0);
-  st_.t[4] = (unsigned long long)(wg_gene[w + 1] - wg_gene[w]);
-  st_.mark(3);
-  st_.flush(0, ((long long)b * gridDim.x + w) * NW + wv, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1324,9 +964,10 @@ __device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const do
 
 // Y part: thread (g, x) = item sums component x of gene g's Y entries [yptr[g], yptr[g + 1]) in
 // entry order, YU loads in flight (a hub gene has many entries).
-template <int K, int YU = FT<K>::YU>
+template <int K>
 __device__ __forceinline__ void genes_ysum(const double* __restrict__ yb, const int* __restrict__ yptr,
                                            long long item, int P, double* __restrict__ ysum_b) {
+  constexpr int YU = FT<K>::YU;
   if (item >= (long long)P * K) return;
   const int g = (int)(item / K), x = (int)(item % K);
   const int e0 = yptr[g], e1 = yptr[g + 1];
@@ -1350,27 +991,7 @@ __global__ __launch_bounds__(256) void ysum_kernel(const double* __restrict__ yb
                                                    double* __restrict__ ysum, int P, long long n_y) {
   const int b = blockIdx.y;
   const long long item = (long long)blockIdx.x * 256 + threadIdx.x;
-  genes_ysum<K>(ybuf + (size_t)b * (n_y + YPAD) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
-}
-
-// The Y sums beside gm_kernel on a second stream (MMSBM_YCONC=1): a small grid (YC_WG workgroups
-// per CU) walking the (gene, component) items with a stride, so its waves fit next to one gm
-// workgroup per CU instead of filling every CU before gm's workgroups are placed.
-#ifndef MMSBM_YC_WG
-#define MMSBM_YC_WG 4
-#endif
-#ifndef MMSBM_YC_YU
-#define MMSBM_YC_YU 16
-#endif
-constexpr int YC_WG = MMSBM_YC_WG;
-template <int K>
-__global__ __launch_bounds__(256) void ysum_gs_kernel(const double* __restrict__ ybuf, const int* __restrict__ yptr,
-                                                      double* __restrict__ ysum, int P, long long n_y) {
-  const int b = blockIdx.y;
-  const double* __restrict__ yb = ybuf + (size_t)b * (n_y + YPAD) * y_stride(K);
-  for (long long item = (long long)blockIdx.x * 256 + threadIdx.x; item < (long long)P * K;
-       item += (long long)gridDim.x * 256)
-    genes_ysum<K, MMSBM_YC_YU>(yb, yptr, item, P, ysum + (size_t)b * P * K);
+  genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
 }
 
 template <int K>
@@ -1420,7 +1041,7 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>
     st_.flush(3, ((long long)b * gridDim.x + w) * NW + wv, lane);
   } else {
     const long long item = ya * FT<K>::NT + tid;
-    genes_ysum<K>(ybuf + (size_t)b * (n_y + YPAD) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
+    genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
   }
 }
 
@@ -1448,7 +1069,7 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(4))) 
                     spart + ((size_t)b * n_sp + sp) * T::K3, Ms, ig, tid, wv, hi, blk, lo, st_);
   } else {
     const long long item = (long long)(w - n_sp_wg) * FT<K>::NT + tid;
-    genes_ysum<K>(ybuf + (size_t)b * (n_y + YPAD) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
+    genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
   }
 }
 
@@ -1478,13 +1099,6 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(4))) 
 #ifndef MMSBM_GM
 #define MMSBM_GM 1
 #endif
-// cell groups per part from 9 chunks (K >= 24), and the occupancy hint above K = 16 (1: free)
-#ifndef MMSBM_GM_CS
-#define MMSBM_GM_CS 2
-#endif
-#ifndef MMSBM_GM_WPE
-#define MMSBM_GM_WPE 1
-#endif
 // gm_kernel occupancy hint: 4 waves per SIMD (<= 128 VGPRs, two 72 KB workgroups per CU) where
 // that does not spill (K <= 16); above, the S accumulators and staging take up to 254 VGPRs and the
 // hint is free (one workgroup per CU; 128 spilled 58-120 VGPRs at K = 20-32)
@@ -1495,7 +1109,7 @@ struct GM {
   static constexpr int AP = 16 * NA;
   static constexpr int RT = 64, CW = 64;     // rows per row tile, cells per chunk
   static constexpr int NCH = (K2 + CW - 1) / CW;
-  static constexpr int CS = NCH > 8 ? MMSBM_GM_CS : 1;    // cell groups (workgroups) per part
+  static constexpr int CS = NCH > 8 ? 2 : 1;              // cell groups (workgroups) per part
   static constexpr int CPG = (NCH + CS - 1) / CS;         // chunks per group
   static constexpr int TST = AP == 32 ? 48 : 16;  // theta tile row stride (= 16 mod 32 doubles)
   static constexpr int XT = 4 * NA, XK = 8 / XT;  // X tiles per row tile, k-splits per tile
@@ -1505,7 +1119,7 @@ struct GM {
   static constexpr int NP = (AP * CW / MW + 511) / 512;
   static constexpr int NTH = RT * AP / 512;       // theta staging loads per thread
   static constexpr int LDS = (RT * CW + AP * CW + RT * TST) * 8;
-  static constexpr int WPE = K <= 16 ? 4 : MMSBM_GM_WPE;
+  static constexpr int WPE = K <= 16 ? 4 : 1;
   static_assert(XT * XK == 8 && ST * SK == 8, "gm: 8 waves");
   static_assert(RT * CW % (MW * 512) == 0 && RT * AP % 512 == 0, "gm staging");
 };
@@ -1737,7 +1351,7 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
         }
       if (ybuf) {  // the gene's Y entries, summed here (no ysum launch): entry order, 8 loads in flight
         constexpr int YU = FT<K>::YU, YS = y_stride(K);
-        const double* __restrict__ yb = ybuf + (size_t)b * (n_y + YPAD) * YS + a;
+        const double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * YS + a;
         const int e0 = yptr[g], e1 = yptr[g + 1];
         double Y = 0.0;
         for (int e = e0; e < e1; e += YU) {
@@ -1989,7 +1603,6 @@ struct Launch {
   int (*mapply)(mmsbm_ctx*, double*, double*, const double*, const double*, hipStream_t);
   int (*predict)(mmsbm_ctx*, const int*, long long, const double*, const double*, double*, hipStream_t);
   int gmax;
-  int gmax16;      // pass16_kernel's gene cap (K = 17-32; 0 below)
   PassFn sk_pass;  // small-K kernels (sk.h), K <= 12; nullptr above
   FinFn sk_fin;
 };
@@ -2045,9 +1658,7 @@ struct mmsbm_ctx {
   bool gsplit = true;
   // large-K M-step contractions in gm_kernel (round 5); MMSBM_GM=0: round 4's gene kernel (measurement)
   bool gm = MMSBM_GM != 0;
-  bool a16 = false;              // K >= MMSBM_A16 (large K): pass16_kernel, 16-row blocks
   bool yupd = true;              // gm path: Y sums inside upd_kernel (MMSBM_YUPD=0: own launch)
-  bool yconc = false;            // gm path: Y sums on a second stream beside gm_kernel (MMSBM_YCONC=1)
   double* xrows = nullptr;       // gm_kernel's X rows [B][n_prows][K]
   hipStream_t ys = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -2095,7 +1706,7 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   // large-K: Y entries (+ the dummy entry of padding rows), M^0 partial rows, S partials, x0 and
   // ysum, likelihood partials, fin's sums-out scratch
   L.cbuf = off;
-  off += align_up(B * (tr.n_y + YPAD) * y_stride(c->K) * 8);
+  off += align_up(B * (tr.n_y + 1) * y_stride(c->K) * 8);
   L.prows = off;
   off += align_up(B * std::max<long long>(tr.n_prows, 1) * K2 * 8);
   L.spart = off;
@@ -2108,8 +1719,8 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   off += align_up(B * (size_t)c->P * c->K * 8);
   L.S = off;
   off += align_up(B * c->R * K3 * 8);
-  L.xrows = off;  // gm_kernel's X rows, one set per cell group (GM<K>::CS <= MMSBM_GM_CS)
-  off += align_up((size_t)MMSBM_GM_CS * B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
+  L.xrows = off;  // gm_kernel's X rows: two cell groups at most (GM<K>::CS)
+  off += align_up(2 * B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
   L.total = off;
   return L;
 }
@@ -2166,29 +1777,10 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
     }
     if (c->gm) {  // round 5: gm_kernel (X rows + S partials in one pass), then the Y sums
       if ((rc = lds_opt_in(c, 10, &gm_kernel<K>, GM<K>::LDS))) return rc;
-      if (c->yconc) {  // the HBM-bound Y sums on a second stream, beside the MFMA-bound gm_kernel
-        if (!c->ys) {
-          HIP_TRY(hipStreamCreateWithFlags(&c->ys, hipStreamNonBlocking));
-          HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-          HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-        }
-        HIP_TRY(hipEventRecord(c->ev_fork, s));
-      }
       gm_kernel<K><<<dim3(std::max(h.n_sp, 1) * GM<K>::CS, nb_of(c)), 512, GM<K>::LDS, s>>>(
           theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, h.n_prows,
           std::max(h.n_sp, 1), (long long)c->B * h.n_prows * K);
       HIP_TRY(hipGetLastError());
-      if (c->yconc) {  // (enqueued after gm, so gm's workgroups are placed first)
-        HIP_TRY(hipStreamWaitEvent(c->ys, c->ev_fork, 0));
-        int ncu = 256;
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
-        ysum_gs_kernel<K><<<dim3((unsigned)(YC_WG * ncu), nb_of(c)), 256, 0, c->ys>>>(c->cbuf, sd.yptr, c->gx + pk,
-                                                                                    c->P, h.n_y);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(c->ev_join, c->ys));
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
-        return MMSBM_OK;
-      }
       if (!c->yupd) {  // MMSBM_YUPD=0 (measurement): the Y sums as a launch of their own
         const long long nyb = ((long long)c->P * K + 255) / 256;
         ysum_kernel<K><<<dim3((unsigned)nyb, nb_of(c)), 256, 0, s>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
@@ -2221,17 +1813,7 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
     if (h.n_wg_a == 0) return MMSBM_OK;
     // dynamic LDS for the context's gene cap (<= the compile-time GMAX the opt-in covers)
     const int lds = (c->gcap * T::VDBL + T::tg_dbl(c->gcap)) * 8 + T::IMG_BYTES + 64;
-    if (mode == PASS_A && c->a16 && h.blk == 4) {  // (MMSBM_BALANCE=0 plans keep 4-row runs)
-      if constexpr (K > 16) {
-        using Q = P16<K>;
-        if ((rc = lds_opt_in(c, 11, &pass16_kernel<K>, Q::LDS))) return rc;
-        const int lds16 = (c->gcap * Q::VDBL + Q::tg_dbl(c->gcap)) * 8 + Q::IMG_BYTES + 64;
-        pass16_kernel<K><<<dim3(h.n_wg_a, nb_of(c)), NT, lds16, s>>>(
-            sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.row_y, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
-            theta, pr, c->cbuf, c->prows, c->P, c->R, h.n_y, h.n_prows, h.n_wg_a, c->eps, c->gcap,
-            h.merge ? 1 : 0);
-      }
-    } else if (mode == PASS_A) {
+    if (mode == PASS_A) {
       if ((rc = lds_opt_in(c, 0, &pass_kernel<K, PASS_A>, T::LDS_A))) return rc;
       pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, nb_of(c)), NT, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.row_y, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
@@ -2267,7 +1849,7 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
   const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
   const double* xr = c->gm ? c->xrows : nullptr;  // gm_kernel's X rows, or gene_kernel's x0
   // gm path: the theta workgroups sum each gene's Y entries themselves (round 5)
-  const double* yb = (c->gm && c->yupd && !c->yconc) ? c->cbuf : nullptr;
+  const double* yb = (c->gm && c->yupd) ? c->cbuf : nullptr;
   if (sums)
     upd_kernel<K, true><<<dim3(nthw + ncw, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
@@ -2388,17 +1970,11 @@ constexpr FinFn sk_fin_fn() {
   else return nullptr;
 }
 
-template <int K>
-constexpr int gmax16_of() {
-  if constexpr (K > 16 && K <= 32) return P16<K>::GMAX;
-  else return 0;
-}
-
 template <int... Ks>
 constexpr auto make_table(std::integer_sequence<int, Ks...>) {
   return std::array<Launch, sizeof...(Ks)>{Launch{&launch_pass<Ks + 1>, &launch_fin<Ks + 1>,
                                                   &launch_mapply<Ks + 1>, &launch_predict<Ks + 1>,
-                                                  KT<Ks + 1>::GMAX, gmax16_of<Ks + 1>(), sk_pass_fn<Ks + 1>(),
+                                                  KT<Ks + 1>::GMAX, sk_pass_fn<Ks + 1>(),
                                                   sk_fin_fn<Ks + 1>()}...};
 }
 
@@ -2410,7 +1986,6 @@ PassFn pass_of(const mmsbm_ctx* c) { return c->sk ? kTable[c->K - 1].sk_pass : k
 FinFn fin_of(const mmsbm_ctx* c) { return c->sk ? kTable[c->K - 1].sk_fin : kTable[c->K - 1].fin; }
 
 int gmax_for(int K) { return kTable[K - 1].gmax; }
-int gmax16_for(int K) { return kTable[K - 1].gmax16; }
 
 int check_shape(const mmsbm_ctx* c) {
   if (c->K < 1 || c->K > MMSBM_MAX_K)
@@ -2513,7 +2088,6 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   if (const char* gsp = getenv("MMSBM_GSPLIT")) c->gsplit = gsp[0] != '0';
   if (const char* gme = getenv("MMSBM_GM")) c->gm = gme[0] != '0';
   if (const char* yu = getenv("MMSBM_YUPD")) c->yupd = yu[0] != '0';
-  if (const char* yc = getenv("MMSBM_YCONC")) c->yconc = yc[0] != '0';
   if (MMSBM_STAMP && getenv("MMSBM_STAMP")) {
     DeviceGuard g(device);
     const size_t bytes = sizeof(unsigned long long) * 5 * STAMP_WAVES * STAMP_SLOTS;
@@ -2599,19 +2173,7 @@ int mmsbm_set_shape(mmsbm_ctx* c, int32_t K, int32_t R, int32_t B, int32_t P, do
   c->warm = false;
   // genes per stream-0 workgroup: the LDS budget's GMAX; MMSBM_GCAP=n lowers it (measurement:
   // smaller V tables let more workgroups share a CU)
-  {
-    int kmin = MMSBM_A16;  // MMSBM_A16=k: pass16_kernel from K = k (0: never; measurement)
-    if (const char* e = getenv("MMSBM_A16")) kmin = atoi(e);
-    const bool a16 = !c->sk && kmin > 0 && K >= kmin && K > 16;
-    if (a16 != c->a16) {  // the plans pad runs differently: set links again
-      DeviceGuard g(c->device);
-      for (auto& sd : c->sets) sd.release();
-      c->ws = nullptr;
-      c->ws_bytes = 0;
-    }
-    c->a16 = a16;
-  }
-  c->gcap = c->a16 ? gmax16_for(K) : gmax_for(K);
+  c->gcap = gmax_for(K);
   if (const char* g = getenv("MMSBM_GCAP")) {
     const int v = atoi(g);
     if (v >= 4 && v < c->gcap) c->gcap = v;
@@ -2679,7 +2241,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   const int sp_cap = (!c->sk && c->gm) ? (1 << 30) : 256;
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
                            c->gcap, sp_rows, c->sk, 1024, c->sk_fused,
-                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge, sp_cap, c->a16 ? 4 : 1);
+                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge, sp_cap);
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
   sd.unit_target = c->sk_fused ? units_a : 0;

@@ -85,7 +85,6 @@ struct Plan {
   std::vector<int> prow_g;         // [n_prows] gene-major position of each partial row
   std::vector<int> gptr;           // [P + 1] each gene's range of gene-major positions
   bool merge = false;              // large-K: one partial row per (workgroup, gene) (see build)
-  int blk = 1;                     // stream-0 runs padded to blk chunks (4: pass16_kernel blocks)
   int rounds_a = 1, rounds_b = 1;  // unit rounds per workgroup (stream 0 / streams 1, 2)
   long long n_units = 0;
   // slot layout the small-K kernels read (make_slots below); group 0 = stream 0 (pass A), group 1 =
@@ -150,16 +149,13 @@ inline void pack_units(const std::vector<int>& run_chunks, int lmax, int gcap, s
 // workgroup lives as long as its longest wave: with one run per unit (pack_units at K = 30 on 10M
 // links: ~5 genes of ~50 chunks per workgroup) 3 of the 8 waves had nothing to do.
 // Returns NW unit boundaries per workgroup (units may be empty when a workgroup has < NW chunks).
-// blk: unit and workgroup boundaries at multiples of blk chunks (the runs are multiples of blk and so
-// is lmax; the 16-observation blocks of the K >= 25 pass kernel, pass16_kernel).
-inline void pack_balanced(const std::vector<int>& run_chunks, int lmax, int gcap, std::vector<int>& ub,
-                          int blk = 1) {
+inline void pack_balanced(const std::vector<int>& run_chunks, int lmax, int gcap, std::vector<int>& ub) {
   ub.assign(1, 0);
   const int cap = NW * std::max(lmax, 1);
   int pos = 0, cur = 0, genes = 0, w0 = 0;
   auto close = [&]() {
-    const long long n = (pos - w0) / blk;
-    for (int i = 1; i <= NW; ++i) ub.push_back(w0 + blk * (int)(i * n / NW));
+    const long long n = pos - w0;
+    for (int i = 1; i <= NW; ++i) ub.push_back(w0 + (int)(i * n / NW));
     w0 = pos;
     cur = 0;
     genes = 0;
@@ -264,7 +260,7 @@ inline void make_slots(Plan& pl) {
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
                   int wg_target = 1024, bool fill = false, int gu = GU, int rho_pct = 85,
-                  bool yent = false, bool balance = true, bool merge = false, int sp_cap = 256, int blk = 1) {
+                  bool yent = false, bool balance = true, bool merge = false, int sp_cap = 256) {
   Plan pl;
   pl.merge = merge && balance && !small && em;
   pl.gu = std::max(1, std::min(gu, GU));
@@ -272,11 +268,6 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   pl.P = P;
   // large-K EM plans, and small-K EM plans with `yent` (sk.h SK_Y): stream 0 + Y entries
   const bool ymode = em && (!small || yent);
-  // stream-0 pivot runs padded to multiples of RP0 rows (blk chunks): blk = 4 gives the 16-row blocks
-  // of pass16_kernel (large K, balanced units only)
-  blk = (!small && balance) ? std::max(1, blk) : 1;
-  pl.blk = blk;
-  const int RP0 = CH * blk;
   pl.streams = (em && !ymode) ? 3 : 1;
   pl.small = small;
   // observations of each rating in link order
@@ -313,8 +304,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
         const int g = ids[(size_t)o[q] * 3 + s];
         size_t q1 = q;
         while (q1 < o.size() && ids[(size_t)o[q1] * 3 + s] == g) ++q1;
-        const int rp = s == 0 ? RP0 : CH;
-        nch += (long long)((q1 - q + rp - 1) / rp) * (rp / CH);
+        nch += (long long)((q1 - q + CH - 1) / CH);
         q = q1;
       }
       (s == 0 ? chunks_a : chunks_b) += nch;
@@ -328,7 +318,6 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
   // 55 / 70 / 85 / 100 on fold0 K=10, profiles/r03ad_rho_ab.txt), streams 1 / 2 at least one block.
   const long long LCAP = small ? LCAP_SK : 64;
   int lmax_a = (int)std::min(LCAP, std::max<long long>(2, (chunks_a + units_a - 1) / std::max(units_a, 1)));
-  lmax_a = (lmax_a + blk - 1) / blk * blk;
   int lmax_b = (int)std::min(LCAP, std::max<long long>(2, (chunks_b + units_b - 1) / std::max(units_b, 1)));
   if (small && fill) {
     const double rho = std::max(10, std::min(100, rho_pct)) / 100.0;
@@ -368,8 +357,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
           pl.rows.push_back(rec);
         }
         const int n = (int)(q1 - q);
-        const int rp = s == 0 ? RP0 : CH;
-        const int pad = (rp - n % rp) % rp;
+        const int pad = (CH - n % CH) % CH;
         for (int t = 0; t < pad; ++t) pl.rows.push_back(I4{g, g, g, s == 0 ? 0 : -2});
         run_chunks.push_back((n + pad) / CH);
         run_gene.push_back(g);
@@ -379,7 +367,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       std::vector<int> ub;
       const bool bal = balance && !small && s == 0;  // units NW per workgroup, even lengths
       if (bal)
-        pack_balanced(run_chunks, lmax_a, gcap, ub, blk);
+        pack_balanced(run_chunks, lmax_a, gcap, ub);
       else
         pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? pl.gu : s == 0 ? gcap : (1 << 30), ub,
                    small && fill);
@@ -513,7 +501,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
           size_t q1 = q;
           while (q1 < o.size() && ids[(size_t)o[q1] * 3] == g) ++q1;
           for (size_t t = q; t < q1; ++t) m[o[t]] = (int)(rr++);
-          rr += (RP0 - (long long)(q1 - q) % RP0) % RP0;
+          rr += (CH - (long long)(q1 - q) % CH) % CH;
           q = q1;
         }
         pl.n_rows0 = (long long)pl.rows.size();
