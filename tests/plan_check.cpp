@@ -242,10 +242,12 @@ int main() {
   // PLAN_MERGE=1: one partial row per (workgroup, gene) (the K >= 25 pass kernel merges its waves' parts)
   const bool merge = getenv("PLAN_MERGE") != nullptr;
   const int gu = (gcap == 0 || gcap == -2) ? 4 : 8;
+  // PLAN_NW=n: n units per large-K workgroup (the K >= 25 pass kernel runs 4-wave workgroups)
+  const int nw_env = getenv("PLAN_NW") ? atoi(getenv("PLAN_NW")) : NW;
   const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill, gu,
                                 85, yent)
                         : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows, false, 1024,
-                                false, GU, 85, false, balance, merge);
+                                false, GU, 85, false, balance, merge, 256, nw_env);
   if (fill) {  // every unit but the last of its (stream, rating) section is full: LCAP_SK chunks or GU stretches
     for (long long u = 0; u + 1 < pl.n_units; ++u) {
       const int* d = &pl.udesc[(size_t)u * UD];
@@ -290,6 +292,8 @@ int main() {
   }
 
   if (small) return check_small(pl, R, P, nch);
+  const int NW = pl.nw;  // units per large-K workgroup
+  if (NW != nw_env) return fail("plan nw", NW, nw_env);
 
   // 2. a chunk has one pivot gene; pivots ascend inside each (stream, rating) section
   // 3. workgroups: NW + 1 nondecreasing unit bounds, units at most 64 chunks, stream-0

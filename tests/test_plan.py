@@ -113,3 +113,17 @@ def test_balanced_plan_fewer_workgroups(plan_check):
     bal = _check(plan_check, 500, 40000, (64, 64), 5, 120, 0.0)
     old = _check(plan_check, 500, 40000, (64, 64), 5, 120, 0.0, env={"PLAN_NO_BALANCE": "1"})
     assert int(bal[3]) < int(old[3])
+
+
+# 4-unit workgroups (the K >= 25 pass kernel: 4-wave workgroups, three per CU, gene cap 4), merged
+# and plain partial rows, balanced and round-3 packing
+@pytest.mark.parametrize("P,E,units,gcap,sp_rows,hub", [
+    (500, 40000, (64, 64), 4, 128, 0.0),
+    (300, 5000, (1536, 3072), 4, 128, 30.0),
+    (40, 600, (1, 1), 4, 16, 0.0),
+    (3000, 4000, (1536, 3072), 4, 128, 0.0),
+])
+@pytest.mark.parametrize("env", [{"PLAN_MERGE": "1"}, {}, {"PLAN_NO_BALANCE": "1"}])
+def test_plan_invariants_four_unit_workgroups(plan_check, P, E, units, gcap, sp_rows, hub, env):
+    out = _check(plan_check, P, E, units, gcap, sp_rows, hub, env={**env, "PLAN_NW": "4"})
+    assert int(out[2]) == 4 * int(out[3])  # units = 4 x workgroups

@@ -86,7 +86,28 @@ int fail(int code, const char* fmt, ...) {
 #ifndef MMSBM_LDS_BIG
 #define MMSBM_LDS_BIG 25
 #endif
-constexpr int lds_target(int K) { return K >= MMSBM_LDS_BIG ? 150 * 1024 : K <= 16 ? 76 * 1024 : 78 * 1024; }
+// Waves per pass workgroup from K = MMSBM_LDS_BIG (MMSBM_PNW): at 130-140 VGPRs a SIMD holds three
+// waves, so 8-wave workgroups run one per CU (two waves per SIMD); 4-wave workgroups with a third of
+// the LDS run three per CU (three per SIMD).  Below LDS_BIG the workgroup keeps NW = 8 waves.
+#ifndef MMSBM_PNW
+#define MMSBM_PNW 4
+#endif
+#ifndef MMSBM_PNW_U
+#define MMSBM_PNW_U 4
+#endif
+#ifndef MMSBM_PNW_DT
+#define MMSBM_PNW_DT 1
+#endif
+#ifndef MMSBM_PNW_WPE
+#define MMSBM_PNW_WPE 3
+#endif
+#ifndef MMSBM_LDS_BIGKB
+#define MMSBM_LDS_BIGKB (MMSBM_PNW == 8 ? 150 : 52)
+#endif
+constexpr int pnw_for(int K) { return K >= MMSBM_LDS_BIG ? MMSBM_PNW : NW; }
+constexpr int lds_target(int K) {
+  return K >= MMSBM_LDS_BIG ? MMSBM_LDS_BIGKB * 1024 : K <= 16 ? 76 * 1024 : 78 * 1024;
+}
 
 // Pass-A ablations for measurement builds only (results invalid): 1 = no Y stores, 2 = theta
 // gathers from 64 hot rows (L2 hits), 4 = no partial-row stores
@@ -154,7 +175,10 @@ struct KT {
   static constexpr int SW = (K % 2 == 0) ? 2 : 1;  // staging width: double2 pieces when K is even
   static constexpr int NPC = (8 * KP / SW + 63) / 64;  // staged pieces per lane per chunk
   static constexpr int IMGW = 2 * IMG + 2;        // per wave: double buffer + a dummy piece slot
-  static constexpr int IMG_BYTES = NW * IMGW * 8;
+  static constexpr int NWK = pnw_for(K), NTK = 64 * NWK;  // pass_kernel's waves / threads
+  // occupancy hint: 4-wave workgroups three per CU (<= 168 VGPRs), else PASS_WPE
+  static constexpr int WPE = NWK == 4 ? MMSBM_PNW_WPE : PASS_WPE;
+  static constexpr int IMG_BYTES = NWK * IMGW * 8;
   static constexpr int GMAX_RAW = (lds_target(K) - IMG_BYTES - 64 - 8) / ((VDBL + TGR) * 8);
   static constexpr int GMAX = GMAX_RAW > 64 ? 64 : (GMAX_RAW < 4 ? 4 : GMAX_RAW);
   static constexpr int LDS_A = GMAX * VDBL * 8 + tg_dbl(GMAX) * 8 + IMG_BYTES + 64;
@@ -168,6 +192,7 @@ struct KT {
 };
 
 int gmax_for(int K);  // host view of KT<K>::GMAX (table below)
+int pnw_host(int K) { return pnw_for(K); }
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
@@ -348,7 +373,7 @@ __device__ __forceinline__ void s_partial(const double* __restrict__ th, const d
 // and per gene stretch the M^0 partial row (K^2) for X^0 and S (gene_kernel).
 // ------------------------------------------------------------------------------------------
 template <int K, int MODE>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) void pass_kernel(
+__global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K>::WPE))) void pass_kernel(
     const int4* __restrict__ rows, const int* __restrict__ chunk_prow,
     const int* __restrict__ chunk_vslot, const int* __restrict__ row_y, const int* __restrict__ wg_units,
     const int* __restrict__ wg_code, const int* __restrict__ wg_gene, const int* __restrict__ vgenes,
@@ -365,7 +390,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   const double* __restrict__ th = theta + (size_t)b * P * K;
   Stamp st_{};
   st_.mark(0);
-  const long long wave_id = ((long long)b * gridDim.x + w) * NW + wv;
+  const long long wave_id = ((long long)b * gridDim.x + w) * T::NWK + wv;
 
   const int code = wg_code[w];
   const int r = code & 15;
@@ -382,10 +407,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   // the other lanes read them by readlane / shuffle, so no register array is indexed at run time.
   // Ring of U record registers: the loop below is unrolled U times so each ring slot keeps a
   // fixed register (a rotation by register moves would wait for every load in flight).
-  constexpr int U = 6;   // records U - 1 chunks ahead
-  constexpr int DT = 2;  // theta values DT chunks ahead (ring of U slots, DT + 1 live)
+  constexpr int U = T::NWK == 4 ? MMSBM_PNW_U : 6;  // records U - 1 chunks ahead
+  constexpr int DT = T::NWK == 4 ? MMSBM_PNW_DT : 2;  // theta values DT chunks ahead (ring of U slots, DT + 1 live)
   constexpr bool EM = MODE == PASS_A;
-  const int c0 = wg_units[w * (NW + 1) + wv], c1 = wg_units[w * (NW + 1) + wv + 1];
+  const int c0 = wg_units[w * (T::NWK + 1) + wv], c1 = wg_units[w * (T::NWK + 1) + wv + 1];
   const int* __restrict__ rows_i = reinterpret_cast<const int*>(rows);
   // Every load in the chunk loop is issued by every lane on every path (addresses clamped, values
   // selected afterwards): an exec-masked load behind a branch would make the compiler's vmcnt
@@ -406,7 +431,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   constexpr bool MG = EM && K >= MMSBM_LDS_BIG;
   bool first_cont = false, last_cont = false;
   if (MG && merge && any) {
-    const int wc0 = wg_units[w * (NW + 1)], wc1 = wg_units[w * (NW + 1) + NW];
+    const int wc0 = wg_units[w * (T::NWK + 1)], wc1 = wg_units[w * (T::NWK + 1) + T::NWK];
     first_cont = c0 > wc0 && __builtin_amdgcn_readfirstlane(chunk_prow[c0 - 1]) ==
                                  __builtin_amdgcn_readfirstlane(chunk_prow[c0]);
     last_cont = c1 < wc1 && __builtin_amdgcn_readfirstlane(chunk_prow[c1]) ==
@@ -423,33 +448,33 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
     // wg_gene; p_r is staged in the image region when it fits.  All loads go out together.
     const int ng = wg_gene[w + 1] - wg_gene[w];
     const int* __restrict__ vgw = vgenes + (size_t)w * gcap;
-    constexpr bool PV = T::K3 <= NW * T::IMGW;
+    constexpr bool PV = T::K3 <= T::NWK * T::IMGW;
     double* Ps = smem + gcap * T::VDBL + T::tg_dbl(gcap);
-    constexpr int NTG = (T::GMAX * T::KP + NT - 1) / NT, NPV = PV ? (T::K3 + NT - 1) / NT : 1;
+    constexpr int NTG = (T::GMAX * T::KP + T::NTK - 1) / T::NTK, NPV = PV ? (T::K3 + T::NTK - 1) / T::NTK : 1;
     double tg[NTG], pv[NPV];
 #pragma unroll
     for (int i = 0; i < NTG; ++i) {
-      const int idx = tid + NT * i, gl = idx / T::KP, a = idx % T::KP;
+      const int idx = tid + T::NTK * i, gl = idx / T::KP, a = idx % T::KP;
       const int g = vgw[gl < gcap ? gl : 0];
       tg[i] = th[(size_t)g * K + (a < K ? a : 0)];
     }
     if constexpr (PV) {
 #pragma unroll
-      for (int i = 0; i < NPV; ++i) pv[i] = p[tid + NT * i < T::K3 ? tid + NT * i : 0];
+      for (int i = 0; i < NPV; ++i) pv[i] = p[tid + T::NTK * i < T::K3 ? tid + T::NTK * i : 0];
     }
     constexpr int ZR = (T::VROWS - K) * VR;  // rows b >= K read as zero
     if constexpr (ZR > 0)
-      for (int idx = tid; idx < ng * ZR; idx += NT)
+      for (int idx = tid; idx < ng * ZR; idx += T::NTK)
         Vt[(idx / ZR) * T::VDBL + K * VR + idx % ZR] = 0.0;
 #pragma unroll
     for (int i = 0; i < NTG; ++i) {  // theta rows, zero padded
-      const int idx = tid + NT * i, gl = idx / T::KP, a = idx % T::KP;
+      const int idx = tid + T::NTK * i, gl = idx / T::KP, a = idx % T::KP;
       if (idx < gcap * T::KP) Tg[gl * T::TGR + a] = (gl < ng && a < K) ? tg[i] : 0.0;
     }
     if constexpr (PV) {
 #pragma unroll
       for (int i = 0; i < NPV; ++i)
-        if (tid + NT * i < T::K3) Ps[tid + NT * i] = pv[i];
+        if (tid + T::NTK * i < T::K3) Ps[tid + T::NTK * i] = pv[i];
     }
     const double* __restrict__ pv_src = PV ? Ps : p;
     __syncthreads();
@@ -458,7 +483,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
     constexpr int CG = (CT + 3) / 4;
     const int GT = (ng + 3) / 4;
     constexpr int GTM = (T::GMAX + 3) / 4;
-    // wave wv owns cell groups (4 cell tiles) cg = wv, wv + NW, ..., CPR per round, for every
+    // wave wv owns cell groups (4 cell tiles) cg = wv, wv + T::NWK, ..., CPR per round, for every
     // gene tile: each p value is loaded once and feeds GT MFMAs (A = the tile's theta rows)
     constexpr int CPR = K <= 12 ? 1 : 2;
     // software pipeline over the rounds: the next round's p values (from L2 when K > 12) are in
@@ -467,8 +492,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
     auto v_load = [&](int cr, double (&bv)[CPR][NG], int (&ctv)[CPR]) {
 #pragma unroll
       for (int u = 0; u < CPR; ++u) {
-        const int ct = 4 * (cr + u * NW) + blk;
-        const bool cv = cr + u * NW < CG && ct < CT;
+        const int ct = 4 * (cr + u * T::NWK) + blk;
+        const bool cv = cr + u * T::NWK < CG && ct < CT;
         const int bb = cv ? ct / NG : 0, hh = cv ? 4 * (ct % NG) + lo : 0;
         ctv[u] = cv ? ct : -1;
 #pragma unroll
@@ -499,7 +524,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
         }
       }
     };
-    constexpr int CST = CPR * NW;  // cell groups per round (all waves)
+    constexpr int CST = CPR * T::NWK;  // cell groups per round (all waves)
     double bvA[CPR][NG], bvB[CPR][NG];
     int ctA[CPR], ctB[CPR];
     v_load(wv, bvA, ctA);
@@ -688,8 +713,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   }
   st_.mark(2);
   if constexpr (MG) {
-    if (merge) {  // (workgroup-uniform) the V tables and images are dead: NW slots of K^2 words
-      static_assert((4 * T::VDBL + T::tg_dbl(4)) * 8 + T::IMG_BYTES >= NW * T::K2 * 8,
+    if (merge) {  // (workgroup-uniform) the V tables and images are dead: T::NWK slots of K^2 words
+      static_assert((4 * T::VDBL + T::tg_dbl(4)) * 8 + T::IMG_BYTES >= T::NWK * T::K2 * 8,
                     "merge slots within the smallest gene cap's LDS");
       const int col = lane & 15;
       __syncthreads();
@@ -707,8 +732,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
       __syncthreads();
       if (kept) {
         const int mypr = __builtin_amdgcn_readfirstlane(chunk_prow[c1 - 1]);
-        for (int nx = wv + 1; nx < NW; ++nx) {  // the continuing waves, in order
-          const int n0 = wg_units[w * (NW + 1) + nx], n1 = wg_units[w * (NW + 1) + nx + 1];
+        for (int nx = wv + 1; nx < T::NWK; ++nx) {  // the continuing waves, in order
+          const int n0 = wg_units[w * (T::NWK + 1) + nx], n1 = wg_units[w * (T::NWK + 1) + nx + 1];
           if (n0 == n1) continue;  // (an empty unit)
           if (__builtin_amdgcn_readfirstlane(chunk_prow[n0]) != mypr) break;
 #pragma unroll
@@ -741,14 +766,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PASS_WPE))) 
   st_.t[4] = (unsigned long long)(wg_gene[w + 1] - wg_gene[w]);
   if constexpr (MODE == PASS_LL) {
     // fixed-order workgroup sum of the log-likelihood terms
-    __shared__ double red[NW];
+    __shared__ double red[T::NWK];
     ll = wave_sum(ll);
     __syncthreads();
     if (lane == 0) red[wv] = ll;
     __syncthreads();
     if (tid == 0) {
       double t = 0.0;
-      for (int q = 0; q < NW; ++q) t += red[q];
+      for (int q = 0; q < T::NWK; ++q) t += red[q];
       partL[(size_t)b * n_wg + w] = t;
     }
   }
@@ -1815,13 +1840,13 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
     const int lds = (c->gcap * T::VDBL + T::tg_dbl(c->gcap)) * 8 + T::IMG_BYTES + 64;
     if (mode == PASS_A) {
       if ((rc = lds_opt_in(c, 0, &pass_kernel<K, PASS_A>, T::LDS_A))) return rc;
-      pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, nb_of(c)), NT, lds, s>>>(
+      pass_kernel<K, PASS_A><<<dim3(h.n_wg_a, nb_of(c)), T::NTK, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, sd.row_y, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
           theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, h.n_y, h.n_prows, h.n_wg_a, c->eps, c->gcap,
           h.merge ? 1 : 0);
     } else {
       if ((rc = lds_opt_in(c, 1, &pass_kernel<K, PASS_LL>, T::LDS_A))) return rc;
-      pass_kernel<K, PASS_LL><<<dim3(h.n_wg_a, nb_of(c)), NT, lds, s>>>(
+      pass_kernel<K, PASS_LL><<<dim3(h.n_wg_a, nb_of(c)), T::NTK, lds, s>>>(
           sd.rows, sd.chunk_prow, sd.chunk_vslot, nullptr, sd.wg_units, sd.wg_code, sd.wg_gene, sd.vgenes,
           theta, pr, c->cbuf, c->prows, c->partL, c->P, c->R, 0, h.n_prows, h.n_wg_a, c->eps, c->gcap, 0);
     }
@@ -2241,7 +2266,7 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   const int sp_cap = (!c->sk && c->gm) ? (1 << 30) : 256;
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
                            c->gcap, sp_rows, c->sk, 1024, c->sk_fused,
-                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge, sp_cap);
+                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge, sp_cap, pnw_host(c->K));
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
   sd.unit_target = c->sk_fused ? units_a : 0;
@@ -2585,7 +2610,7 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[7] = h.small ? h.gu : h.gmax;
   info[8] = h.small ? info[9] : (int64_t)h.vgenes.size();  // small-K: one V table per stream-0 stretch
   info[10] = h.small ? (c->sk_y ? 3 : c->sk_fused ? 2 : 1) : 0;
-  info[11] = h.small ? h.n_units : (int64_t)(h.n_wg_a + h.n_wg_b) * NW;
+  info[11] = h.small ? h.n_units : (int64_t)(h.n_wg_a + h.n_wg_b) * h.nw;
   info[12] = c->sets[which].ncu;
   info[13] = c->sets[which].unit_target;
   info[14] = h.n_y;

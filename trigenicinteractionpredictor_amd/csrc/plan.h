@@ -60,7 +60,7 @@ struct Plan {
   std::vector<I4> rows;            // all streams, stream-major then rating-major
   std::vector<int> chunk_prow;     // partial row of each chunk (-1: likelihood-only plan)
   std::vector<int> chunk_vslot;    // stream 0: the chunk's pivot gene in its workgroup's gene list
-  std::vector<int> wg_units;       // [n_wg][NW + 1] chunk boundaries of the workgroup's units
+  std::vector<int> wg_units;       // [n_wg][nw + 1] chunk boundaries of the workgroup's units
   std::vector<int> wg_code;        // [n_wg] stream * 16 + rating
   std::vector<int> wg_gene;        // [n_wg + 1] offsets into vgenes (stream-0 workgroups)
   std::vector<int> vgenes;         // pivot genes of each stream-0 workgroup, ascending
@@ -85,6 +85,7 @@ struct Plan {
   std::vector<int> prow_g;         // [n_prows] gene-major position of each partial row
   std::vector<int> gptr;           // [P + 1] each gene's range of gene-major positions
   bool merge = false;              // large-K: one partial row per (workgroup, gene) (see build)
+  int nw = NW;                     // units (waves) per large-K workgroup (small-K plans: NW)
   int rounds_a = 1, rounds_b = 1;  // unit rounds per workgroup (stream 0 / streams 1, 2)
   long long n_units = 0;
   // slot layout the small-K kernels read (make_slots below); group 0 = stream 0 (pass A), group 1 =
@@ -149,13 +150,14 @@ inline void pack_units(const std::vector<int>& run_chunks, int lmax, int gcap, s
 // workgroup lives as long as its longest wave: with one run per unit (pack_units at K = 30 on 10M
 // links: ~5 genes of ~50 chunks per workgroup) 3 of the 8 waves had nothing to do.
 // Returns NW unit boundaries per workgroup (units may be empty when a workgroup has < NW chunks).
-inline void pack_balanced(const std::vector<int>& run_chunks, int lmax, int gcap, std::vector<int>& ub) {
+inline void pack_balanced(const std::vector<int>& run_chunks, int lmax, int gcap, std::vector<int>& ub,
+                          int nw = NW) {
   ub.assign(1, 0);
-  const int cap = NW * std::max(lmax, 1);
+  const int cap = nw * std::max(lmax, 1);
   int pos = 0, cur = 0, genes = 0, w0 = 0;
   auto close = [&]() {
     const long long n = pos - w0;
-    for (int i = 1; i <= NW; ++i) ub.push_back(w0 + (int)(i * n / NW));
+    for (int i = 1; i <= nw; ++i) ub.push_back(w0 + (int)(i * n / nw));
     w0 = pos;
     cur = 0;
     genes = 0;
@@ -260,8 +262,10 @@ inline void make_slots(Plan& pl) {
 inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R, int P, bool em,
                   int units_a, int units_b, int gcap, int sp_rows = 16, bool small = false,
                   int wg_target = 1024, bool fill = false, int gu = GU, int rho_pct = 85,
-                  bool yent = false, bool balance = true, bool merge = false, int sp_cap = 256) {
+                  bool yent = false, bool balance = true, bool merge = false, int sp_cap = 256,
+                  int nw = NW) {
   Plan pl;
+  pl.nw = small ? NW : std::max(1, std::min(nw, NW));
   pl.merge = merge && balance && !small && em;
   pl.gu = std::max(1, std::min(gu, GU));
   pl.R = R;
@@ -367,7 +371,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
       std::vector<int> ub;
       const bool bal = balance && !small && s == 0;  // units NW per workgroup, even lengths
       if (bal)
-        pack_balanced(run_chunks, lmax_a, gcap, ub);
+        pack_balanced(run_chunks, lmax_a, gcap, ub, pl.nw);
       else
         pack_units(run_chunks, s == 0 ? lmax_a : lmax_b, small ? pl.gu : s == 0 ? gcap : (1 << 30), ub,
                    small && fill);
@@ -415,13 +419,13 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
         // workgroups: NW consecutive units; stream 0 also caps the distinct genes (V table)
         std::vector<int> wstart;  // unit index where each workgroup starts
         if (bal) {
-          for (int u = 0; u < nunits; u += NW) wstart.push_back(u);
+          for (int u = 0; u < nunits; u += pl.nw) wstart.push_back(u);
         } else {
           int u = 0;
           while (u < nunits) {
             wstart.push_back(u);
             int taken = 0, genes = 0, last = -1;
-            while (u < nunits && taken < NW) {
+            while (u < nunits && taken < pl.nw) {
               int ug = 0, lg = last;
               for (int c = ub[u]; c < ub[u + 1]; ++c)
                 if (cgene[c] != lg) {
@@ -439,7 +443,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
         for (size_t w = 0; w < wstart.size(); ++w) {
           const int u0 = wstart[w];
           const int u1 = w + 1 < wstart.size() ? wstart[w + 1] : nunits;
-          for (int i = 0; i <= NW; ++i) {
+          for (int i = 0; i <= pl.nw; ++i) {
             const int u = std::min(u0 + i, u1);
             pl.wg_units.push_back(chunk_base + ub[u]);
           }
@@ -469,7 +473,7 @@ inline Plan build(const int32_t* ids, const int32_t* counts, long long E, int R,
         int u = 0;
         for (int c = 0; c < nch; ++c) {
           while (u + 1 < (int)ub.size() && ub[u + 1] <= c) ++u;
-          const int start = (bal && merge) ? ub[(u / NW) * NW] : ub[u];
+          const int start = (bal && merge) ? ub[(u / pl.nw) * pl.nw] : ub[u];
           if (c == start || cgene[c] != cgene[c - 1]) {
             pl.prow_gene.push_back(cgene[c]);
             ++pl.n_prows;
