@@ -12,6 +12,7 @@ import json
 import sys
 
 NAMES = {"pass_kernel<%d, 0>": "pass_a", "gene_kernel<%d>": "gene", "upd_kernel<%d, false>": "fin",
+         "gm_kernel<%d>": "gene",  # (large-K X rows + S partials, round 5: the gene label)
          "ysum_kernel<%d>": "ysum",  # (large-K Y sums, on a second stream beside gene_kernel)
          "gene_sy_kernel<%d>": "gene_sy",  # (large-K S + Y workgroups, the gene label's second launch)
          # small-K kernels (csrc/sk.h), labelled as EMEngine.LABELS names them
