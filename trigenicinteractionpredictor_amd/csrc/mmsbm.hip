@@ -1345,10 +1345,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
 // ------------------------------------------------------------------------------------------
 constexpr int UPD_NT = 512;
 
-// Y entries in flight per upd thread (entry order either way, so the bits do not depend on it)
-#ifndef MMSBM_UPD_YU
-#define MMSBM_UPD_YU 8
-#endif
 template <int K, bool SUMS>
 __global__ __launch_bounds__(UPD_NT) void upd_kernel(
     double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ x0,
@@ -1378,8 +1374,8 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
           for (int h = 1; h < GM<K>::CS; ++h) x += xb[h * xgs + (size_t)q * K];
           X += x;
         }
-      if (ybuf) {  // the gene's Y entries, summed here (no ysum launch): entry order, YU loads in flight
-        constexpr int YU = MMSBM_UPD_YU, YS = y_stride(K);
+      if (ybuf) {  // the gene's Y entries, summed here (no ysum launch): entry order, 8 loads in flight
+        constexpr int YU = FT<K>::YU, YS = y_stride(K);
         const double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * YS + a;
         const int e0 = yptr[g], e1 = yptr[g + 1];
         double Y = 0.0;
