@@ -93,17 +93,6 @@ struct SKT {
   static_assert(16 * NCG <= SLOT + SK_ROWS + THL, "S operand reads past the slots and records");
 };
 
-// n / d by v_rcp_f64 and two Newton steps plus a residual correction (within an ulp or two of the
-// IEEE quotient; d > 0 here): a shorter dependent chain than the IEEE division's scale / fixup
-// sequence in the chunk loop.  Deterministic, so results stay bitwise reproducible.
-__device__ __forceinline__ double sk_div(double n, double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  r = fma(fma(-d, r, 1.0), r, r);
-  r = fma(fma(-d, r, 1.0), r, r);
-  const double q = n * r;
-  return fma(fma(-d, q, n), r, q);
-}
-
 // p index of P^s[z][cell] (s = the pivot slot z sits in; cell = x K + y over the two other
 // slots u, v in order): s = 0 p[z][x][y], s = 1 p[x][z][y], s = 2 p[x][y][z]
 template <int K>
