@@ -86,11 +86,17 @@ int fail(int code, const char* fmt, ...) {
 #ifndef MMSBM_LDS_BIG
 #define MMSBM_LDS_BIG 25
 #endif
-// Waves per pass workgroup from K = MMSBM_LDS_BIG (MMSBM_PNW): at 130-140 VGPRs a SIMD holds three
-// waves, so 8-wave workgroups run one per CU (two waves per SIMD); 4-wave workgroups with a third of
-// the LDS run three per CU (three per SIMD).  Below LDS_BIG the workgroup keeps NW = 8 waves.
+// Waves per pass workgroup from K = MMSBM_LDS_BIG (MMSBM_PNW; below LDS_BIG always NW = 8) and
+// the V operands in registers (MMSBM_VREG, pass_kernel).  Measured at K=30 on 10M links, one box
+// (profiles/r05_vreg_ab.txt): 8-wave workgroups with V in registers (~245 VGPRs, one workgroup per
+// CU) are fastest; 4-wave workgroups (MMSBM_PNW=4: 52 KB, three per CU at <= 168 VGPRs with U=4 /
+// DT=1, profiles/r05_pnw4_ab.txt) beat 8-wave ones only while V is read from LDS, and with V in
+// registers (two per CU) they lose.
 #ifndef MMSBM_PNW
-#define MMSBM_PNW 4
+#define MMSBM_PNW 8
+#endif
+#ifndef MMSBM_VREG
+#define MMSBM_VREG 1
 #endif
 #ifndef MMSBM_PNW_U
 #define MMSBM_PNW_U 4
@@ -605,6 +611,11 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
 
   // w of observation hi (its count n_r) of a record register
   auto rec_w = [&](int rr) { return __shfl(rr, hi * 4 + 3, 64); };
+  // VREG (MMSBM_VREG, K >= MMSBM_LDS_BIG): the pivot gene's Z / Z' operands of the V table kept in
+  // registers for the whole stretch (reloaded at a gene change) instead of read from LDS per chunk
+  constexpr bool VREG = MMSBM_VREG && K >= MMSBM_LDS_BIG && EM;
+  double vz[VREG ? T::NBG : 1][VREG ? NG : 1], vzp[VREG ? T::NBG : 1][VREG ? NG : 1];
+  int cur_vs = -1;
   if (any) {
     // Software pipeline: records U - 1 chunks ahead, theta values DT ahead; the LDS image of
     // chunk q + 1 is written at the end of chunk q (double buffer).
@@ -629,7 +640,20 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
 
         // ---- Z[obs hi][b] for b = 4 (4 bg + blk) + lo, then d, c
         const int nw = rec_w(rq);
-        const double* __restrict__ V = Vt + __builtin_amdgcn_readlane(rq, 17) * T::VDBL;
+        const int vsl = __builtin_amdgcn_readlane(rq, 17);
+        const double* __restrict__ V = Vt + vsl * T::VDBL;
+        if constexpr (VREG) {
+          if (vsl != cur_vs) {  // (uniform) a new pivot gene: its V operands into registers
+            cur_vs = vsl;
+#pragma unroll
+            for (int bg = 0; bg < T::NBG; ++bg)
+#pragma unroll
+              for (int hs = 0; hs < NG; ++hs) {
+                vz[bg][hs] = V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi];
+                vzp[bg][hs] = V[(4 * hs + hi) * VR + 16 * bg + 4 * blk + lo];
+              }
+          }
+        }
         double az[NG];  // th_v[obs lo][4 hs + hi]: the A operand of every b group
 #pragma unroll
         for (int hs = 0; hs < NG; ++hs) az[hs] = I[(4 + lo) * TR + 4 * hs + hi];
@@ -640,7 +664,7 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
           double z = 0.0;
 #pragma unroll
           for (int hs = 0; hs < NG; ++hs)
-            z = mfma4(az[hs], V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
+            z = mfma4(az[hs], VREG ? vz[bg][hs] : V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
           zb[bg] = z;
           dp = fma(I[hi * TR + 16 * bg + 4 * blk + lo], z, dp);
         }
@@ -668,7 +692,7 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
             // KP reach only Y pad words, which nothing reads)
 #pragma unroll
             for (int bs = 0; bs < NG; ++bs)
-              z2 = mfma4(au[bs], V[(4 * bs + hi) * VR + 16 * hg + 4 * blk + lo], z2);
+              z2 = mfma4(au[bs], VREG ? vzp[hg][bs] : V[(4 * bs + hi) * VR + 16 * hg + 4 * blk + lo], z2);
             const int hh = 16 * hg + 4 * blk + lo;
             if (hh < YS && !(MMSBM_ABL & 1)) yb[(size_t)e2 * YS + hh] = c * z2;
             else if (MMSBM_ABL & 1) ll += z2;  // (keep Z' live)
