@@ -98,6 +98,9 @@ int fail(int code, const char* fmt, ...) {
 #ifndef MMSBM_VREG
 #define MMSBM_VREG 1
 #endif
+#ifndef MMSBM_VREG_MIN
+#define MMSBM_VREG_MIN MMSBM_LDS_BIG
+#endif
 #ifndef MMSBM_PNW_U
 #define MMSBM_PNW_U 4
 #endif
@@ -611,9 +614,9 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
 
   // w of observation hi (its count n_r) of a record register
   auto rec_w = [&](int rr) { return __shfl(rr, hi * 4 + 3, 64); };
-  // VREG (MMSBM_VREG, K >= MMSBM_LDS_BIG): the pivot gene's Z / Z' operands of the V table kept in
+  // VREG (MMSBM_VREG, K >= MMSBM_VREG_MIN = MMSBM_LDS_BIG): the pivot gene's Z / Z' operands of the V table kept in
   // registers for the whole stretch (reloaded at a gene change) instead of read from LDS per chunk
-  constexpr bool VREG = MMSBM_VREG && K >= MMSBM_LDS_BIG && EM;
+  constexpr bool VREG = MMSBM_VREG && K >= MMSBM_VREG_MIN && EM;
   double vz[VREG ? T::NBG : 1][VREG ? NG : 1], vzp[VREG ? T::NBG : 1][VREG ? NG : 1];
   int cur_vs = -1;
   if (any) {
