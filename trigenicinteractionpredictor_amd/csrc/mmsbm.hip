@@ -98,6 +98,9 @@ int fail(int code, const char* fmt, ...) {
 #ifndef MMSBM_VREG
 #define MMSBM_VREG 1
 #endif
+#ifndef MMSBM_ZSPLIT
+#define MMSBM_ZSPLIT 0
+#endif
 #ifndef MMSBM_VREG_MIN
 #define MMSBM_VREG_MIN MMSBM_LDS_BIG
 #endif
@@ -617,6 +620,7 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
   // VREG (MMSBM_VREG, K >= MMSBM_VREG_MIN = MMSBM_LDS_BIG): the pivot gene's Z / Z' operands of the V table kept in
   // registers for the whole stretch (reloaded at a gene change) instead of read from LDS per chunk
   constexpr bool VREG = MMSBM_VREG && K >= MMSBM_VREG_MIN && EM;
+  constexpr bool ZSPLIT = MMSBM_ZSPLIT && K > 16;
   double vz[VREG ? T::NBG : 1][VREG ? NG : 1], vzp[VREG ? T::NBG : 1][VREG ? NG : 1];
   int cur_vs = -1;
   if (any) {
@@ -664,10 +668,15 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
         double dp = 0.0;
 #pragma unroll
         for (int bg = 0; bg < T::NBG; ++bg) {
-          double z = 0.0;
+          // MMSBM_ZSPLIT: even and odd h steps in two accumulators (shorter dependent MFMA chains)
+          double z = 0.0, zo = 0.0;
 #pragma unroll
-          for (int hs = 0; hs < NG; ++hs)
-            z = mfma4(az[hs], VREG ? vz[bg][hs] : V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi], z);
+          for (int hs = 0; hs < NG; ++hs) {
+            const double vv = VREG ? vz[bg][hs] : V[(16 * bg + 4 * blk + lo) * VR + 4 * hs + hi];
+            if (ZSPLIT && (hs & 1)) zo = mfma4(az[hs], vv, zo);
+            else z = mfma4(az[hs], vv, z);
+          }
+          if (ZSPLIT) z += zo;
           zb[bg] = z;
           dp = fma(I[hi * TR + 16 * bg + 4 * blk + lo], z, dp);
         }
@@ -690,12 +699,16 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
           }
 #pragma unroll
           for (int hg = 0; hg < T::NBG; ++hg) {
-            double z2 = 0.0;
+            double z2 = 0.0, z2o = 0.0;
             // (columns h in [K, KP) of V are zero; the pad column and the next row's words past
             // KP reach only Y pad words, which nothing reads)
 #pragma unroll
-            for (int bs = 0; bs < NG; ++bs)
-              z2 = mfma4(au[bs], VREG ? vzp[hg][bs] : V[(4 * bs + hi) * VR + 16 * hg + 4 * blk + lo], z2);
+            for (int bs = 0; bs < NG; ++bs) {
+              const double vv = VREG ? vzp[hg][bs] : V[(4 * bs + hi) * VR + 16 * hg + 4 * blk + lo];
+              if (ZSPLIT && (bs & 1)) z2o = mfma4(au[bs], vv, z2o);
+              else z2 = mfma4(au[bs], vv, z2);
+            }
+            if (ZSPLIT) z2 += z2o;
             const int hh = 16 * hg + 4 * blk + lo;
             if (hh < YS && !(MMSBM_ABL & 1)) yb[(size_t)e2 * YS + hh] = c * z2;
             else if (MMSBM_ABL & 1) ll += z2;  // (keep Z' live)
