@@ -99,7 +99,7 @@ int fail(int code, const char* fmt, ...) {
 #define MMSBM_VREG 1
 #endif
 #ifndef MMSBM_ZSPLIT
-#define MMSBM_ZSPLIT 0
+#define MMSBM_ZSPLIT 1
 #endif
 #ifndef MMSBM_VREG_MIN
 #define MMSBM_VREG_MIN MMSBM_LDS_BIG
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
   // VREG (MMSBM_VREG, K >= MMSBM_VREG_MIN = MMSBM_LDS_BIG): the pivot gene's Z / Z' operands of the V table kept in
   // registers for the whole stretch (reloaded at a gene change) instead of read from LDS per chunk
   constexpr bool VREG = MMSBM_VREG && K >= MMSBM_VREG_MIN && EM;
-  constexpr bool ZSPLIT = MMSBM_ZSPLIT && K > 16;
+  constexpr bool ZSPLIT = MMSBM_ZSPLIT && K >= MMSBM_VREG_MIN;  // (K = 20: -7 %, r05_zsplit_ab.txt)
   double vz[VREG ? T::NBG : 1][VREG ? NG : 1], vzp[VREG ? T::NBG : 1][VREG ? NG : 1];
   int cur_vs = -1;
   if (any) {
