@@ -10,6 +10,7 @@ import random
 import pytest
 
 from oracle.mmsbm_oracle import OracleModel
+from trigenicinteractionpredictor_amd.launch import free_port
 from trigenicinteractionpredictor_amd import cli
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tiny")
@@ -258,7 +259,7 @@ def test_two_rank_gloo_cli_writes_the_one_rank_files(tmp_path):
     assert rc == 0
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() + 250) % 1000
+    port = free_port()  # (a pid-derived port collided with another xdist worker's test)
     argv = base + ["-o", str(two) + os.sep]
     procs = [ctx.Process(target=_ranked_worker, args=(r, 2, port, argv, q)) for r in range(2)]
     for p in procs:
@@ -296,7 +297,7 @@ def test_two_ranks_without_seed_replay_rank0_stream(tmp_path):
     assert rc == 0
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() + 410) % 1000
+    port = free_port()
     procs = [ctx.Process(target=_ranked_worker, args=(r, 2, port, base + ["-o", str(two) + os.sep], q, 4100))
              for r in range(2)]
     for p in procs:

@@ -13,6 +13,7 @@ import torch.multiprocessing as mp
 
 from oracle.mmsbm_oracle import OracleModel
 from oracle_engine import OracleEngine
+from trigenicinteractionpredictor_amd.launch import free_port
 from trigenicinteractionpredictor_amd.model import Model
 from trigenicinteractionpredictor_amd.restarts import (fixed_run, gather_rows, init_samples,
                                                        replay_check, result_rows, rows_digest,
@@ -98,7 +99,7 @@ def _worker(rank, world, port, queue):
 def test_two_rank_gloo_gather_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000
+    port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -135,7 +136,7 @@ def _fixed_worker(rank, world, port, queue):
 def test_two_rank_fixed_run_digest_equals_one_rank_and_replay():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() + 500) % 1000
+    port = free_port()
     procs = [ctx.Process(target=_fixed_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
