@@ -95,7 +95,7 @@ def spawn_ranks(n):
 
 KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, Z', d, c, the j / k Y entries, M0 "
                           "partial rows; FP64 MFMA)",
-                "gene": "gene_kernel<%d> (X0 contractions on FP64 MFMA) + gene_sy_kernel (S partials, Y entry sums)",
+                "gene": "gm_kernel<%d> (X rows and S partials from the M0 partial rows, FP64 MFMA)",
                 "fused": "fused E-step: sky_pass_kernel<%d> (SK_Y, stream 0: V, Z, Z', d, c, Y entries, "
                          "M, X, S partials) / sk_pass_kernel<K, SK_U> (3 streams); FP64 MFMA",
                 "pass_b": "sk_pass_kernel<%d, SK_B> (streams 1/2: M1, M2, X)",
@@ -176,9 +176,11 @@ def s8d_work(K, P, R, B, E_obs):
 
 
 def pmc_traffic(build_id, K, E_obs, B):
-    """HBM bytes per launch / per iteration from a PMC record under profiles/ taken with THIS
-    build (tools/pmc_to_traffic.py stamps each record with the profiled library's build id);
-    None when no record names this build."""
+    """L2->fabric bytes per launch from a PMC record under profiles/ taken with THIS build
+    (tools/pmc_to_traffic.py stamps each record with the profiled library's build id, and states
+    its basis: Infinity-Cache hits included, FETCH doubled for wide-stream kernels only); None when
+    no record names this build.  Round-5 records (HBM-labelled, FETCH doubled everywhere) are
+    not used."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
@@ -188,7 +190,7 @@ def pmc_traffic(build_id, K, E_obs, B):
         except (OSError, ValueError):
             continue
         if (rec.get("build_id") == build_id and rec.get("K") == K and rec.get("E_obs") == E_obs
-                and rec.get("B") == B and rec.get("hbm_bytes_per_launch")):
+                and rec.get("B") == B and rec.get("l2_fabric_bytes_per_launch")):
             best = (os.path.relpath(f, REPO), rec)
     return best
 
@@ -209,7 +211,7 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
     pmc = pmc_traffic(build_id, K, E_obs, B)
     traffic = None
     if pmc is not None:
-        traffic = sum(pmc[1]["hbm_bytes_per_launch"].get(k, 0.0) for k in work)
+        traffic = sum(pmc[1]["l2_fabric_bytes_per_launch"].get(k, 0.0) for k in work)
     exe_tf = exe / iter_s / 1e12
     # the 8d credit counts the reference's 8 K^3 per observation; where that exceeds the FP64
     # peak (K >= 20 here: the factorisation does far less work) it says nothing about utilisation,
@@ -224,7 +226,12 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
                            "executed FLOPs (the 8d credit exceeds the FP64 peak)"),
             "credited": {"achieved": tf, "frac": tf / FP64_PEAK_TFLOPS},
             "traffic": traffic,
-            "traffic_unit": "HBM bytes per iteration (PMC FETCH_SIZE x 2 + WRITE_SIZE, all kernels)",
+            "traffic_unit": "L2->fabric bytes per iteration, all kernels (PMC FETCH_SIZE + WRITE_SIZE: "
+                            "Infinity-Cache hits included, so an upper bound on HBM bytes; FETCH x 2 "
+                            "only for wide-stream kernels)",
+            "traffic_basis": None if pmc is None else pmc[1].get("basis"),
+            "traffic_per_kernel": None if pmc is None else pmc[1]["l2_fabric_bytes_per_launch"],
+            "tcc_hit_rate": None if pmc is None else pmc[1].get("tcc_hit_rate"),
             "traffic_source": None if pmc is None else pmc[0],
             "traffic_build_id": None if pmc is None else pmc[1]["build_id"],
             "per": "one EM iteration of all %d sample(s): %.4g FLOPs credited by SURVEY 8d "
@@ -240,7 +247,7 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
                                 "tflops": dfl / dom_s / 1e12, "mfma_frac": dfl / dom_s / 1e12 / FP64_PEAK_TFLOPS,
                                 "gbs": dby / dom_s / 1e9, "hbm_frac": dby / dom_s / 1e9 / HBM_PEAK_GBS,
                                 "traffic_per_launch": None if pmc is None else
-                                pmc[1]["hbm_bytes_per_launch"].get(dom)}}
+                                pmc[1]["l2_fabric_bytes_per_launch"].get(dom)}}
 
 
 def make_fold(P, E, rank, hub="", test_frac=0.2):
@@ -365,9 +372,10 @@ def main():
         launch_check(args, world, rank)
         return 0
     if args.backend == "nccl" and world > 1:
-        from trigenicinteractionpredictor_amd.launch import visible_gpus
-        if world > visible_gpus():   # RCCL: one GPU per rank of a communicator
-            print("bench.py: %d nccl ranks need %d GPUs, %d visible" % (world, world, visible_gpus()),
+        import torch               # (a rank: it uses its GPU anyway)
+        n_vis = torch.cuda.device_count()
+        if world > n_vis:          # RCCL: one GPU per rank of a communicator
+            print("bench.py: %d nccl ranks need %d GPUs, %d visible" % (world, world, n_vis),
                   file=sys.stderr)
             return 2
     train, test = make_fold(args.P, args.E, rank, args.hub, args.test_frac)

@@ -153,7 +153,9 @@ int mmsbm_set_theta_addend(mmsbm_ctx *ctx, const double *nth_add);
  * fused E-step launch, pass A then runs all three streams and pass B is empty; 0: the large-K
  * kernels), units (waves of work), [12] the compute-unit count the fused plan sized its units
  * from (0: the plan does not depend on it), [13] that plan's unit target, [14] Y entries of the
- * large-K plan (2 per observation), [15] reserved (0).  The fused plan's unit length, and so the
+ * large-K plan (2 per observation), [15] the large-K gm_kernel's workgroups per S part for the
+ * current active batch (1 or 2; it follows the batch, the bits do not: its X rows are formed in
+ * two fixed halves either way; 0 on the small-K plans).  The fused plan's unit length, and so the
  * order of its sums, follows [12]: results are bitwise reproducible on one device model /
  * partition mode. */
 int mmsbm_plan_info(const mmsbm_ctx *ctx, int32_t which, int64_t *info);

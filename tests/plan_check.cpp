@@ -244,10 +244,12 @@ int main() {
   const int gu = (gcap == 0 || gcap == -2) ? 4 : 8;
   // PLAN_NW=n: n units per large-K workgroup (the K >= 25 pass kernel runs 4-wave workgroups)
   const int nw_env = getenv("PLAN_NW") ? atoi(getenv("PLAN_NW")) : NW;
+  // PLAN_SP_CAP=n: at most n S-partial parts per rating (the large-K product plans take 1,024)
+  const int sp_cap = getenv("PLAN_SP_CAP") ? atoi(getenv("PLAN_SP_CAP")) : 256;
   const Plan pl = small ? build(ids.data(), counts.data(), E, R, P, true, ua, ub, 0, 16, true, sp_rows, fill, gu,
                                 85, yent)
                         : build(ids.data(), counts.data(), E, R, P, true, ua, ub, gcap, sp_rows, false, 1024,
-                                false, GU, 85, false, balance, merge, 256, nw_env);
+                                false, GU, 85, false, balance, merge, sp_cap, nw_env);
   if (fill) {  // every unit but the last of its (stream, rating) section is full: LCAP_SK chunks or GU stretches
     for (long long u = 0; u + 1 < pl.n_units; ++u) {
       const int* d = &pl.udesc[(size_t)u * UD];

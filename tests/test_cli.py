@@ -334,3 +334,40 @@ def test_nccl_ranks_beyond_visible_gpus_are_refused(monkeypatch):
     monkeypatch.setattr(launch, "visible_gpus", lambda: 1)
     rc, lines = _run(["--gpus", "2", "-t", TRAIN, "-e", TEST, "-k", "2"])
     assert rc == 2 and any("visible" in l for l in lines)
+
+
+def test_eight_rank_gloo_cli_config3_topology(tmp_path):
+    """BASELINE config 3's topology on CPU: 64 restarts, `--batch 8`, eight
+    gloo ranks (one per GPU of the node in the real run), the C oracle as each rank's engine and
+    the reference's check schedule / convergence rule (:1262-1279).  The Sample files equal a
+    one-process `--batch 8` run's byte for byte, rank 0's gathered summary lists all 64 samples
+    in sample order, and the other ranks print nothing (src/run.sh:36-45, :1253-1279)."""
+    import multiprocessing as mp
+    one, eight = tmp_path / "one", tmp_path / "eight"
+    one.mkdir()
+    eight.mkdir()
+    base = ["-k", "3", "-i", "40", "-n", "64", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST, "--seed", "20",
+            "--batch", "8"]
+    rc, lines1 = _pool_run(base, one)
+    assert rc == 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    argv = base + ["-o", str(eight) + os.sep]
+    procs = [ctx.Process(target=_ranked_worker, args=(r, 8, port, argv, q)) for r in range(8)]
+    for p in procs:
+        p.start()
+    got = {r: (rc, lines) for r, rc, lines in (q.get(timeout=400) for _ in procs)}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(got[r][0] == 0 for r in range(8))
+    assert all(got[r][1] == [] for r in range(1, 8))
+    summary = lambda ls: [l for l in ls if l.startswith("Sample ") and "iterations" in l]  # noqa: E731
+    s8 = summary(got[0][1])
+    assert [int(l.split()[1][:-1]) for l in s8] == list(range(64))
+    assert s8 == summary(lines1)
+    files = sorted(os.listdir(one))
+    assert files and files == sorted(os.listdir(eight))
+    for f in files:
+        assert (one / f).read_bytes() == (eight / f).read_bytes()

@@ -122,6 +122,32 @@ def test_cli_pool_writes_the_sequential_files(tmp_path, monkeypatch, K, env):
     assert st.refills >= 1 and st.slot_iterations == st.sample_iterations
 
 
+def test_cli_default_batch_families_agree_within_tolerance(tmp_path, monkeypatch):
+    """with the default environment a sequential run (the drop-in Model: one sample,
+    SK_U) and a `--batch 4` run (SK_Y) sum in different orders, so their files are not byte
+    equal; they converge after the same iterations and their likelihoods agree to the parity
+    tolerance (the user-visible contract stated in the CLI help and README)."""
+    for k in ("MMSBM_SK_Y", "MMSBM_SK_FUSED", "MMSBM_SK"):
+        monkeypatch.delenv(k, raising=False)
+    seq, bat = tmp_path / "seq", tmp_path / "bat"
+    seq.mkdir()
+    bat.mkdir()
+    base = ["-k", "3", "-i", "80", "-n", "8", "-f", "4", "-b", "6", "-t", TRAIN, "-e", TEST, "--seed", "11"]
+    l1, l2 = [], []
+    with contextlib.redirect_stdout(io.StringIO()):
+        assert cli.main(base + ["-o", str(seq) + os.sep], out=l1.append) == 0
+        assert cli.main(base + ["-o", str(bat) + os.sep, "--batch", "4"], out=l2.append) == 0
+    files = sorted(os.listdir(seq))
+    assert files and files == sorted(os.listdir(bat))
+    its = [l for l in l2 if l.startswith("Sample ") and "iterations" in l]
+    assert sum(int(l.split()[2]) for l in its) == sum(1 for l in l1 if l.startswith("· Iteration "))
+    for f in files:
+        a, b = (seq / f).read_text().split("\n"), (bat / f).read_text().split("\n")
+        assert len(a) == len(b)
+        for x, y in zip(a[:2], b[:2]):  # Max / Held-out likelihood header lines
+            np.testing.assert_allclose(float(x.split("\t")[1]), float(y.split("\t")[1]), rtol=1e-9)
+
+
 @pytest.mark.parametrize("K,family", [(10, "sky"), (13, "auto")])
 def test_pool_results_equal_single_sample_runs(tmp_path, K, family):
     """restarts.run_pool with 4 slots over 10 samples (refills, then shrinking): every sample's

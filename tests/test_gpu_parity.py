@@ -163,14 +163,15 @@ def test_work_plan_splits_match_oracle(tmp_path, monkeypatch, K, units):
     (28, 40, 3000, {"MMSBM_UNITS": "1,1"}),    # 64-chunk units: runs span 3+ waves of a workgroup
     (30, 60, 4000, {"MMSBM_MERGE": "0"}),      # one row per unit stretch (measurement path)
     (30, 60, 4000, {"MMSBM_BALANCE": "0"}),    # whole runs per unit (round-3 packing)
-    (26, 50, 3000, {"MMSBM_GSPLIT": "0"}),     # the gene kernel in one launch
+    (26, 50, 3000, {"MMSBM_SP_ROWS": "8"}),    # many short S-partial parts (gm_kernel row tiles)
+    (20, 60, 4000, {"MMSBM_GCAP": "4"}),       # fewer V-table genes per pass-A workgroup
     (20, 60, 4000, {"MMSBM_UNITS": "1,1"}),    # balanced without merging (K < 25)
 ])
 def test_large_k_plan_variants_match_oracle(tmp_path, monkeypatch, K, P, E, env):
-    """The round-4 large-K work plans (csrc/plan.h pack_balanced, Plan::merge; mmsbm.hip's merged
-    partial rows and split gene launch) with few genes and long pivot runs, so a run's chunks
+    """The large-K work plans (csrc/plan.h pack_balanced, Plan::merge; mmsbm.hip's merged partial
+    rows, gm_kernel's S-partial parts, the pass-A gene cap) with few genes and long pivot runs, so a run's chunks
     spread over several waves of a workgroup, vs the C oracle after 2 iterations."""
-    for k in ("MMSBM_UNITS", "MMSBM_MERGE", "MMSBM_BALANCE", "MMSBM_GSPLIT"):
+    for k in ("MMSBM_UNITS", "MMSBM_MERGE", "MMSBM_BALANCE", "MMSBM_SP_ROWS", "MMSBM_GCAP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -554,7 +555,8 @@ def test_in_place_link_edit_between_iterations_matches_oracle():
                                    (3, {"MMSBM_SK_Y": "1", "MMSBM_UNITS": "7,3"}),
                                    (1, {"MMSBM_SK_Y": "1"}), (2, {"MMSBM_SK_Y": "1"}),
                                    (4, {"MMSBM_SK_Y": "1", "MMSBM_UNITS": "3,3"}),
-                                   (11, {"MMSBM_SK_Y": "1"}), (9, {"MMSBM_SK_Y": "1", "MMSBM_UNITS": "1,1"})])
+                                   (11, {"MMSBM_SK_Y": "1"}), (9, {"MMSBM_SK_Y": "1", "MMSBM_UNITS": "1,1"}),
+                                   (10, {"MMSBM_SK_RHO": "50"}), (6, {"MMSBM_SK_RHO": "100"})])
 def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
     """K <= 12 runs the small-K kernels (csrc/sk.h; the three-stream fused E-step by default
     (SK_U), the stream-0 E-step with Y entries with MMSBM_SK_Y=1 (SK_Y), pass A + pass B with
@@ -581,3 +583,64 @@ def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
     np.testing.assert_allclose(np.array(m.pr), pr_o, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(m.compute_likelihood("train"), L_o, rtol=RTOL)
     np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
+
+
+@pytest.mark.parametrize("K", [13, 16, 20, 22])
+def test_gm_workgroups_per_part_keep_bits(tmp_path, monkeypatch, K):
+    """gm_kernel forms its X rows in two fixed halves of the cell chunks (GM<K>::HALF), so one or
+    two workgroups per S part (MMSBM_GM_CS=1 / 2) give the same bits: the launch may follow the
+    batch.  Both agree bit for bit and with the C oracle."""
+    tr, te = _fold(tmp_path, 150, 2500, seed=K + 40, multi_frac=0.05, both_frac=0.02)
+    out = {}
+    for cs in ("1", "2"):
+        monkeypatch.setenv("MMSBM_GM_CS", cs)
+        m = _gpu_model(tr, te)
+        random.seed(K)
+        m.initialize_parameters(K)
+        theta0, pr0 = np.array(m.theta), np.array(m.pr)
+        m.make_iterations(2)
+        assert m._engine.plan_info()["gm_groups"] == int(cs)
+        out[cs] = (np.array(m.theta), np.array(m.pr), m.compute_likelihood("train"))
+    np.testing.assert_array_equal(out["1"][0], out["2"][0])
+    np.testing.assert_array_equal(out["1"][1], out["2"][1])
+    assert out["1"][2] == out["2"][2]
+    th_o, pr_o, L_o, _ = _oracle_run(m, theta0, pr0, 2)
+    np.testing.assert_allclose(out["1"][0], th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(out["1"][1], pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(out["1"][2], L_o, rtol=RTOL)
+
+
+def test_gm_workgroups_follow_the_batch_with_the_same_bits(tmp_path, monkeypatch):
+    """Without the override gm_kernel takes two workgroups per S part where the doubled grid fits
+    one round of resident workgroups (one sample) and one where it would not (8 samples): a
+    sample run alone and the same sample in slot 3 of an 8-sample engine end bit for bit equal
+    (K=20, ~19 parts)."""
+    from trigenicinteractionpredictor_amd import EMEngine
+    from trigenicinteractionpredictor_amd.layout import links_to_arrays
+    monkeypatch.delenv("MMSBM_GM_CS", raising=False)
+    tr, te = _fold(tmp_path, 1200, 20000, seed=61)
+    m = _gpu_model(tr, te)
+    K, B = 20, 8
+    random.seed(9)
+    thetas, prs = [], []
+    for _ in range(B):
+        m.initialize_parameters(K)
+        thetas.append(np.array(m.theta))
+        prs.append(np.array(m.pr))
+    ids, counts = links_to_arrays(m.links)
+    big = EMEngine(K, m.P, B=B)
+    big.set_links(0, ids, counts)
+    big.upload(np.stack(thetas), np.stack(prs))
+    one = EMEngine(K, m.P, B=1)
+    one.set_links(0, ids, counts)
+    one.upload(thetas[3][None], prs[3][None])
+    g8, g1 = big.plan_info()["gm_groups"], one.plan_info()["gm_groups"]
+    import torch
+    if torch.cuda.get_device_properties(big.device).multi_processor_count == 256:  # (the rule counts CUs)
+        assert (g8, g1) == (1, 2), (g8, g1)
+    big.iterate(2)
+    one.iterate(2)
+    tb, pb = big.download()
+    t1, p1 = one.download()
+    np.testing.assert_array_equal(tb[3], t1[0])
+    np.testing.assert_array_equal(pb[3], p1[0])

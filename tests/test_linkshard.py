@@ -12,6 +12,7 @@ import torch.multiprocessing as mp
 
 from oracle import c_oracle
 from oracle_engine import OracleShardEngine
+from trigenicinteractionpredictor_amd.launch import free_port
 from trigenicinteractionpredictor_amd.linkshard import LinkShardedEM, shard_links, train_degree
 from trigenicinteractionpredictor_amd.model import Model
 from trigenicinteractionpredictor_amd.restarts import run_samples
@@ -114,7 +115,7 @@ def _worker(rank, world, port, queue):
 def test_two_rank_gloo_allreduce_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 28500 + os.getpid() % 1000
+    port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -139,3 +140,50 @@ def test_two_rank_gloo_allreduce_matches_single_process():
                          [0], [th], [pr], iterations=30, fcheck=3, bcheck=4)[0]
     assert got[0][4][:2] == (single.iterations, single.converged)
     np.testing.assert_allclose(got[0][4][2], single.loglik, rtol=1e-12)
+
+
+def _active_worker(rank, world, port, queue):
+    """Three samples; after 3 iterations the active prefix shrinks to 2 (the restart pool retiring
+    slot 2): the collective then reduces the active slots only, so slot 2's stale local sums are
+    never summed again (they grew by the world size each iteration)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _host()
+    ids, counts = c_oracle.links_to_arrays(m.links)
+    tids, tcounts = c_oracle.links_to_arrays(m.test_links)
+    ths, prs = zip(*[_init(m, 3, s) for s in (1, 2, 3)])
+    em = LinkShardedEM(OracleShardEngine(3, m.P, B=3), ids, counts, tids, tcounts)
+    em.upload(np.stack(ths), np.stack(prs))
+    em.iterate(3)
+    em.set_active(2)
+    stale = em.nth[2].clone(), em.S[2].clone()
+    em.iterate(40)
+    t, p = em.download()
+    queue.put((rank, t[:2], p[:2], bool((em.nth[2] == stale[0]).all() and (em.S[2] == stale[1]).all())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_shrunken_active_prefix_reduces_active_slots_only():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_active_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {g[0]: g[1:] for g in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    m = _host()
+    ids, counts = c_oracle.links_to_arrays(m.links)
+    for r in (0, 1):
+        t, p, untouched = got[r]
+        assert untouched
+        for b, s in enumerate((1, 2)):
+            th, pr = _init(m, 3, s)
+            for _ in range(43):
+                th, pr = c_oracle.make_iteration(ids, counts, th, pr)
+            np.testing.assert_allclose(t[b], th, rtol=1e-11, atol=1e-300)
+            np.testing.assert_allclose(p[b], pr, rtol=1e-11, atol=1e-300)

@@ -127,3 +127,16 @@ def test_balanced_plan_fewer_workgroups(plan_check):
 def test_plan_invariants_four_unit_workgroups(plan_check, P, E, units, gcap, sp_rows, hub, env):
     out = _check(plan_check, P, E, units, gcap, sp_rows, hub, env={**env, "PLAN_NW": "4"})
     assert int(out[2]) == 4 * int(out[3])  # units = 4 x workgroups
+
+
+@pytest.mark.parametrize("cap", [3, 16, 1024])
+def test_s_partial_parts_are_capped_per_rating(plan_check, cap):
+    """the large-K S partials take R x parts x K^3 doubles per sample, so their number
+    is capped per rating (mmsbm_set_links: 1,024 with 128 rows a part) whatever E; past the cap
+    the parts grow longer (gm_kernel walks any number of 64-row tiles) and still tile each
+    rating's partial rows (plan_check's S-partial tiling check)."""
+    out = _check(plan_check, 500, 40000, (1536, 3072), 13, 4, 0.0, env={"PLAN_SP_CAP": str(cap)})
+    n_prows, n_sp = int(out[4]), int(out[5])
+    assert n_sp <= 2 * cap
+    if cap < 16:
+        assert n_sp == 2 * cap and n_prows > 4 * n_sp   # capped: longer parts

@@ -102,8 +102,8 @@ PY
   stamp)
     local name=$1 lib=$2; shift 2
     MMSBM_STAMP=1 MMSBM_STAMP_DUMP="$OUT/$name.bin" MMSBM_LIB="$R/$lib" timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --roofline-launches 5 "$@" > "$OUT/$name.json" 2> "$OUT/$name.err" || { echo "stamp $name failed"; tail -5 "$OUT/$name.err"; return 1; }
-    python3 tools/stamp_analyze.py "$OUT/$name.bin" > "$OUT/$name.txt" && rm -f "$OUT/$name.bin"
-    head -40 "$OUT/$name.txt" ;;
+    python3 tools/stamp_analyze.py "$OUT/$name.bin" "$OUT/$name.json" > "$OUT/$name.txt" && rm -f "$OUT/$name.bin"
+    head -60 "$OUT/$name.txt" ;;
   py)
     local name=$1 script=$2; shift 2
     timeout -k 10 600 python -u "$script" "$@" > "$OUT/$name.txt" 2> "$OUT/$name.err" || { echo "py $name failed"; tail -20 "$OUT/$name.err"; return 1; }

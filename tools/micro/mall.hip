@@ -46,6 +46,23 @@ __global__ __launch_bounds__(256) void read_seq(const d2* __restrict__ y, long l
   if (a.x == -1.2345) out[0] = a.y;  // keeps the load
 }
 
+// The guide's load shape (MI355X_MICROARCH.md, indexed rows / Infinity Cache): 16 B per lane and
+// U independent loads in flight per lane (U x 1 KiB per wave; 8 waves per 512-thread workgroup
+// -> 64 KiB per workgroup in flight), the grid sized to a few workgroups per CU and striding
+template <int U>
+__global__ __launch_bounds__(512) void read_seq_u(const d2* __restrict__ y, long long n16, double* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * 512 * U;
+  double acc = 0.0;
+  for (long long base = (long long)blockIdx.x * 512 * U + threadIdx.x; base < n16; base += stride) {
+    d2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = y[base + (long long)u * 512 < n16 ? base + (long long)u * 512 : base];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y;
+  }
+  if (acc == -1.2345) out[0] = acc;  // keeps the loads
+}
+
 template <class F>
 float med_us(F f, int reps) {
   hipEvent_t a, b;
@@ -68,7 +85,7 @@ float med_us(F f, int reps) {
 
 int main() {
   const long long MB = 1 << 20;
-  const long long sizes[] = {16 * MB, 48 * MB, 96 * MB, 128 * MB, 192 * MB, 256 * MB, 512 * MB, 2048 * MB, 5120 * MB};
+  const long long sizes[] = {16 * MB, 38 * MB, 48 * MB, 96 * MB, 128 * MB, 151 * MB, 192 * MB, 256 * MB, 512 * MB, 2048 * MB, 5120 * MB};
   const long long maxb = 5120 * MB;
   d2* y;
   int* perm;
@@ -79,8 +96,8 @@ int main() {
     return 1;
   }
   std::vector<int> h(maxb / 256);
-  printf("%10s %12s %12s %12s %12s %14s %14s\n", "MB", "wr_seq GB/s", "wr_scat GB/s", "rd GB/s", "rd_gath GB/s",
-         "scat+rd GB/s", "seq+gath GB/s");
+  printf("%10s %12s %12s %12s %12s %14s %14s %12s %12s\n", "MB", "wr_seq GB/s", "wr_scat GB/s", "rd GB/s", "rd_gath GB/s",
+         "scat+rd GB/s", "seq+gath GB/s", "rd_u8 GB/s", "rd_u16 GB/s");
   double base_rt = 0;
   std::vector<double> rts;
   for (long long S : sizes) {
@@ -102,9 +119,13 @@ int main() {
       write_seq<<<nb, 256>>>(y, n, 2.0);
       read_gather<<<nb, 256>>>(y, perm, n, out);
     }, 9);
+    // the guide's shape: 16 B per lane, 8 / 16 loads in flight per lane, 4 workgroups per CU
+    const float tu8 = med_us([&] { read_seq_u<8><<<1024, 512>>>(y, n * 16, out); }, 9);
+    const float tu16 = med_us([&] { read_seq_u<16><<<1024, 512>>>(y, n * 16, out); }, 9);
     const double gb = S / 1e9;
-    printf("%10lld %12.0f %12.0f %12.0f %12.0f %14.0f %14.0f\n", S / MB, gb / (tw * 1e-6), gb / (ts * 1e-6),
-           gb / (tr * 1e-6), gb / (tg * 1e-6), 2 * gb / (trt * 1e-6), 2 * gb / (trt2 * 1e-6));
+    printf("%10lld %12.0f %12.0f %12.0f %12.0f %14.0f %14.0f %12.0f %12.0f\n", S / MB, gb / (tw * 1e-6), gb / (ts * 1e-6),
+           gb / (tr * 1e-6), gb / (tg * 1e-6), 2 * gb / (trt * 1e-6), 2 * gb / (trt2 * 1e-6), gb / (tu8 * 1e-6),
+           gb / (tu16 * 1e-6));
     rts.push_back(2 * gb / (trt * 1e-6));
   }
   // ring of two 96 MB regions against one 5 GB stream, same bytes: 52 write+read round trips

@@ -10,7 +10,12 @@ import numpy as np
 NAMES = ["passA", "passB", "fin", "spart", "passLL"]
 
 
-def main(path):
+def main(path, bench_json=None):
+    n_wg0 = None
+    if bench_json:  # the bench line of the same run: stream-0 workgroups come first in the grid
+        import json
+        line = open(bench_json).read().strip().splitlines()[-1]
+        n_wg0 = json.loads(line)["plan"].get("wg_stream0")
     h = np.fromfile(path, dtype=np.uint64).reshape(5, 1 << 16, 10).astype(np.int64)
     for k, name in enumerate(NAMES):
         t = h[k]
@@ -47,6 +52,26 @@ def main(path):
             print("  start (ns from the first wave) %s" % q((t[:, 8] - rt0) * 10))
             print("  end   (ns from the first wave) %s" % q((t[:, 9] - rt0) * 10))
             print("  life  (ns)                     %s" % q((t[:, 9] - t[:, 8]) * 10))
+            if n_wg0:  # per stream group: the chip-wide end time and the phases (cycles)
+                wg = idx // 8
+                for gname, sel in (("stream 0", wg < n_wg0), ("streams 1/2", wg >= n_wg0)):
+                    if not sel.any():
+                        continue
+                    tt = t[sel]
+                    print("  [%s] %d waves" % (gname, sel.sum()))
+                    print("    end ns    %s" % q((tt[:, 9] - rt0) * 10))
+                    print("    life ns   %s" % q((tt[:, 9] - tt[:, 8]) * 10))
+                    print("    prologue  %s" % q(tt[:, 1] - tt[:, 0]))
+                    print("    chunks    %s" % q(tt[:, 2] - tt[:, 1]))
+                    print("    epilogue  %s" % q(tt[:, 3] - tt[:, 2]))
+                    print("    tail      %s" % q(tt[:, 7] - tt[:, 3]))
+                    # what sets a wave's length: its stretches (V reloads, M flushes), its chunks
+                    for ns in np.unique(tt[:, 4]):
+                        sel2 = tt[:, 4] == ns
+                        cl = tt[sel2, 2] - tt[sel2, 1]
+                        print("    stretches %2d: %5d waves, chunks med %3d, chunk loop med %6d p90 %6d, life ns med %6d" % (
+                            ns, sel2.sum(), np.median(tt[sel2, 5]), np.median(cl), np.percentile(cl, 90),
+                            np.median((tt[sel2, 9] - tt[sel2, 8]) * 10)))
             ch = t[:, 5]
             print("  chunks %s  stretches %s" % (q(ch), q(t[:, 4])))
             if ch.max() > 0 and ch.min() < ch.max():
@@ -74,4 +99,4 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)

@@ -25,7 +25,10 @@ sample starts from the state the one-process run gives it, runs with the referen
 schedule and convergence rule (:1262-1279) on its own GPU, and writes its own
 `Sample_<n>_K<k>.csv`.  One all-gather at the end (RCCL over xGMI under nccl) brings every
 sample's result to rank 0, which prints the summary.  A sample's bits depend neither on its batch
-nor on its rank, so the files equal a one-process run's byte for byte.
+nor on its rank, so the files equal a one-process run's byte for byte.  (At K <= 12 the kernel
+family follows `--batch`: B = 1 sums in SK_U's order, B >= 2 in SK_Y's, so files written with
+different `--batch` values agree to ~1e-12 relative, not byte for byte; include/mmsbm.h
+mmsbm_set_family.)
 """
 from __future__ import annotations
 
@@ -42,7 +45,9 @@ python -m trigenicinteractionpredictor_amd.cli [-h|--help] [-i|--num_iterations=
     [-f|--fcheck=] <likelihood check frequency, 0: never> [-b|--bcheck=] <first check after>
     [-o|--out=] <output path prefix> [-t|--train=] <train file> [-e|--test=] <test file>
     [-k|--k=] <number of groups> [--seed=] <RNG seed, default: the process id>
-    [--batch=] <samples advanced together on the GPU, default 1>
+    [--batch=] <samples advanced together on the GPU, default 1; at K <= 12 a batch of 2 or more
+               runs the batched kernel family, whose files agree with --batch 1 to ~1e-12, not
+               byte for byte>
     [--gpus=] <processes, one per GPU, over which the samples are sharded, default 1>
     [--backend=] <collective backend of --gpus: nccl (RCCL, default) or gloo>
 
@@ -281,11 +286,19 @@ def spawn_ranks(n, argv):
 def _too_many_ranks(cfg, out):
     """RCCL takes one GPU per rank: --gpus above the visible GPUs would put two ranks of one
     communicator on one device (refused or hung), so it is an argument error (gloo ranks may
-    share a GPU: a rehearsal mode)."""
+    share a GPU: a rehearsal mode).  The launching parent counts GPUs from sysfs (no HIP call
+    before the ranks exist; launch.visible_gpus); a rank, which uses the GPU anyway, asks the
+    runtime."""
     if cfg["backend"] != "nccl":
         return False
-    from .launch import visible_gpus
-    n = visible_gpus()
+    if "WORLD_SIZE" in os.environ:
+        import torch
+        n = torch.cuda.device_count()
+    else:
+        from .launch import visible_gpus
+        n = visible_gpus()
+        if n is None:          # topology unreadable: the ranks check
+            return False
     if cfg["gpus"] > n:
         out("\n\nERROR: --gpus %d with the nccl backend needs %d GPUs, %d visible (--backend gloo "
             "shares GPUs)" % (cfg["gpus"], cfg["gpus"], n))

@@ -1,8 +1,10 @@
 // mmsbm.hip — MI355X (gfx950) MMSBM EM engine: kernels + C ABI (include/mmsbm.h).
 //
 // Hot path of AleixMT/TrigenicInteractionPredictor, src/TrigenicInteractionPredictor.py:
-//   make_iteration      :984-1043   -> pass_kernel<K, PASS_A>, pass_kernel<K, PASS_B>, fin_kernel<K>
-//   compute_likelihood  :952-974    -> pass_kernel<K, PASS_LL> + reduce_kernel
+//   make_iteration      :984-1043   -> K <= 12 (sk.h): sk_pass_kernel<K, SK_U> (or sky_pass_kernel<K>)
+//                                      + sk_fin_kernel<K>; K > 12: pass_kernel<K, PASS_A>,
+//                                      gm_kernel<K>, upd_kernel<K>
+//   compute_likelihood  :952-974    -> sk_pass_kernel<K, SK_LL> / pass_kernel<K, PASS_LL> + reduce_kernel
 //   do_prediction       :530-547    -> predict_kernel<K>
 //
 // Pivot-run factorisation.  The reference spends K^3 work per observed (link, rating):
@@ -14,19 +16,21 @@
 //   V_g[b][h]   = sum_a th_g[a] p_r[a][b][h]                         per gene (stream 0 only)
 //   Z_o[b]      = sum_h V_g[b][h] th_k(o)[h],  d_o = eps + sum_b th_j(o)[b] Z_o[b],  c_o = n_o / d_o
 //   M^s_g[x][y] = sum_{o with pivot g} c_o th_u(o)[x] th_v(o)[y]      K^2 per observation
-// and per gene (fin_kernel):
+// and per gene (the update kernels):
 //   X^0_g[a] = sum_bh p[a][b][h] M^0_g[b][h],  X^1_g[b] = sum_ah p M^1_g[a][h],  X^2_g[h] = sum_ab p M^2_g[a][b]
 //   theta'_g = theta_g (sum_r X^0 + X^1 + X^2) / deg_g                          (:1009-1018)
 //   S_r = sum_g theta_g (x) M^0_g,  p' = p S / (eps + sum_r p S)               (:1012, :1021-1028)
 // (tests/pivot_model.py restates this in numpy and checks it against the C oracle.)
 //
 // Per observation the GPU does K^2 work (Z, and M for each of the three slots) on FP64 MFMA
-// (v_mfma_f64_4x4x4f64); the K^3 work is per pivot gene.  One EM iteration is three launches:
-//   PASS_A  stream 0 (pivot = slot 0): V in LDS per workgroup, then per 4-observation chunk Z, d,
-//           c (stored), M^0 accumulated in registers and flushed as a partial row per gene stretch
-//   PASS_B  streams 1 and 2: c read back, M^1 / M^2 partial rows; extra workgroups form the S
-//           partials from the M^0 partial rows and snapshot p for fin_kernel
-//   FIN     per gene: partial rows summed in a fixed order, X, theta'; per cell: S summed, p'
+// (v_mfma_f64_4x4x4f64 / 16x16x4f64); the K^3 work is per pivot gene.  A large-K iteration is three
+// launches:
+//   PASS_A  stream 0 (pivot = slot 0): V in LDS per workgroup, then per 4-observation chunk Z, Z',
+//           d, c; the j / k slots' sums as Y entries c Z, c Z'; M^0 flushed as a partial row per
+//           gene stretch
+//   gm      X rows (M^0 p) and S partials (theta (x) M^0) in one pass over the partial rows
+//   upd     per gene: X rows + Y entries summed in a fixed order, theta'; per cell: S summed, p'
+// The small-K family (sk.h) fuses the E-step into one launch per iteration plus its update.
 // Every sum has a fixed order: results are bitwise reproducible run to run.
 
 #include <hip/hip_runtime.h>
@@ -146,21 +150,6 @@ constexpr int y_stride(int K) { return (K + MMSBM_YALIGN - 1) / MMSBM_YALIGN * M
 #endif
 constexpr int PASS_WPE = MMSBM_PASS_WPE;
 
-#ifndef MMSBM_GENE_GT24
-#define MMSBM_GENE_GT24 0
-#endif
-// gene_kernel fill rounds: partial rows per entry loaded together (0 = FT's choice; measurement)
-#ifndef MMSBM_GENE_RW
-#define MMSBM_GENE_RW 0
-#endif
-
-// gene_kernel's workgroup kinds in blockIdx order: gene, S, then Y workgroups (0), or interleaved
-// in proportion over the grid (1, measurement: K=20 x 8 gene kernel 120 vs 74 us, K=30 1,938 vs
-// 1,348 us, profiles/r04n_ablations.txt — the Y workgroups then hold CUs the MFMA-bound kinds need)
-#ifndef MMSBM_GENE_MIX
-#define MMSBM_GENE_MIX 0
-#endif
-
 // Row strides of pass A's V tables and of their genes' theta rows: odd (1) or the round-3 even
 // strides (0, measurement).  The compiler pairs the chunk loop's V reads into ds_read2_b64, whose
 // 16-lane groups bank on (a/4) mod 32: an odd stride puts the 16 rows of a Z read (b = 4 blk + lo)
@@ -198,7 +187,6 @@ struct KT {
   // S partials: (a-tile, group of 4 cell tiles) items over the 8 waves
   static constexpr int NCT = (K2 + 3) / 4;
   static constexpr int NCG = (NCT + 3) / 4;
-  static constexpr int NIG = (NCG + NW - 1) / NW;  // S partial: one cell group per wave, NIG workgroups
   static_assert(LDS_A <= 160 * 1024, "pass A LDS over budget");
   static_assert(64 * KP * 8 <= IMG_BYTES, "S partial staging over the pass B LDS");
 };
@@ -309,84 +297,6 @@ __device__ __forceinline__ double row16_sum(double v) {
 }
 
 enum { PASS_A = 0, PASS_LL = 1, PASS_B = 2 };  // (PASS_B: the small-K family's stream-1/2 pass)
-
-// ------------------------------------------------------------------------------------------
-// S partial of one workgroup (gene_kernel): S_r[a][cell] += th_g(q)[a] M_q[cell] over the partial rows
-// q of stream 0, rating r, in [q0, q1), cells (b, h) dense.  MFMA k index = four partial rows,
-// blocks = four cell tiles; wave wv of item group ig owns cell group cg = ig NW + wv (16 cells)
-// for every a tile, so each partial-row value is loaded once and feeds NG MFMAs.
-// ------------------------------------------------------------------------------------------
-template <int K, int RS>
-__device__ __forceinline__ void s_partial(const double* __restrict__ th, const double* __restrict__ prows_b,
-                                          const int* __restrict__ prow_gene, int q0, int q1,
-                                          double* __restrict__ out, double* __restrict__ Tq, int ig,
-                                          int tid, int wv, int hi, int blk, int lo, Stamp& st_) {
-  using T = KT<K>;
-  constexpr int NG = T::NG;
-  // blocks of QB partial rows: their genes' theta rows staged in LDS (zero padded), so the loop
-  // over the block only streams the partial rows themselves
-  constexpr int QB = 64, NI = (QB * T::KP + NT - 1) / NT;  // (RS: 4-row steps per round)
-  const int cg = ig * NW + wv;
-  const bool cgv = cg < T::NCG;
-  const int cell = 4 * (4 * (cgv ? cg : 0) + blk) + lo;
-  const bool cv = cgv && cell < T::K2;
-  const int cellc = cv ? cell : 0;
-  double acc[NG];
-#pragma unroll
-  for (int t = 0; t < NG; ++t) acc[t] = 0.0;
-  for (int qb = q0; qb < q1; qb += QB) {
-    const int nq = q1 - qb < QB ? q1 - qb : QB;
-    __syncthreads();
-    double x[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int idx = tid + NT * i, ql = idx / T::KP, a = idx % T::KP;
-      const int g = prow_gene[qb + (ql < nq ? ql : 0)];
-      const double v = th[(size_t)g * K + (a < K ? a : 0)];
-      x[i] = (idx < QB * T::KP && ql < nq && a < K) ? v : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-      if (tid + NT * i < QB * T::KP) Tq[tid + NT * i] = x[i];
-    __syncthreads();
-    st_.mark(1);
-    // RS steps of 4 rows per round, double-buffered: the next round's partial-row loads are in
-    // flight during this round's MFMAs.  Rows past nq load row 0 of the block (finite) against
-    // zero theta rows; an invalid cell loads cell 0 and is never stored.
-    auto ldm = [&](int qq, double (&m)[RS]) {
-#pragma unroll
-      for (int u = 0; u < RS; ++u) {
-        const int row = qq + 4 * u + hi;
-        m[u] = prows_b[(size_t)(qb + (row < nq ? row : 0)) * T::K2 + cellc];
-      }
-    };
-    auto mma = [&](int qq, const double (&m)[RS]) {
-#pragma unroll
-      for (int u = 0; u < RS; ++u) {
-        const int row = qq + 4 * u + hi;  // Tq rows past nq (and past QB) read as zero
-        const double* tq = Tq + (row < QB ? row : 0) * T::KP;
-#pragma unroll
-        for (int t = 0; t < NG; ++t) acc[t] = mfma4(row < QB ? tq[4 * t + lo] : 0.0, m[u], acc[t]);
-      }
-    };
-    double mA[RS], mB[RS];
-    ldm(0, mA);
-    for (int qq = 0; qq < nq; qq += 8 * RS) {
-      ldm(qq + 4 * RS, mB);
-      mma(qq, mA);
-      ldm(qq + 8 * RS, mA);
-      if (qq + 4 * RS < nq) mma(qq + 4 * RS, mB);
-    }
-  }
-  if (cgv) {
-#pragma unroll
-    for (int t = 0; t < NG; ++t) {
-      const int a = 4 * t + hi;
-      if (a < K && cell < T::K2) st_wt(out + (size_t)a * T::K2 + cell, acc[t]);
-    }
-  }
-  st_.mark(2);
-}
 
 // ------------------------------------------------------------------------------------------
 // Pass kernel, grid (workgroups, B), block 512 = one unit (contiguous chunks) per wave; stream 0
@@ -837,322 +747,9 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
   st_.flush(MODE == PASS_A ? 0 : 4, wave_id, lane);
 }
 
-// ------------------------------------------------------------------------------------------
-// gene_kernel (the M-step's gene side, launch 2 of an iteration), grid (gene workgroups + S
-// workgroups + Y workgroups, B), block 512:
-//   gene workgroups, 16 genes each (4 MFMA row tiles): for every rating r, the genes' stream-0
-//     partial rows summed into LDS (fixed order), then
-//       X0[g][a] += sum_k M_{r,g}[k] p_r[a][k]    (k = the (b, h) cells, dense)
-//     on FP64 MFMA; wave w takes a group w % NXG and k part w / NXG of all four tiles, so each p
-//     load (from L2) feeds 4 MFMAs; the k parts are added in order.  -> x0[B][P][K]
-//   S workgroups: S_r[a][cell] = sum_q th_g(q)[a] M_q[cell] over ~16 stream-0 partial rows
-//     (s_partial above) -> spart[B][n_sp][K^3]
-//   Y workgroups: thread (g, x) sums gene g's Y entries (contiguous, entry order) -> ysum[B][P][K]
-// Nothing here writes theta or p (upd_kernel does, one launch later), so the S workgroups read
-// the theta the pass used.
-// ------------------------------------------------------------------------------------------
-struct SpRange {
+struct SpRange {  // per rating: the S partials [lo, hi) of the train plan
   int lo[MAX_R], hi[MAX_R];
 };
-
-template <int K>
-struct FT {
-  static constexpr int K2 = K * K, NG = (K + 3) / 4, KP = 4 * NG;
-  static constexpr int KS = (K2 + 3) / 4;       // k-steps over the dense (b, h) cells
-  static constexpr int K2P = 4 * KS;
-  static constexpr int NXG = (NG + 3) / 4;      // MFMA groups of 4 a tiles
-  // gene row tiles per workgroup: 4 (16 genes); -DMMSBM_GENE_GT24=1 takes 2 (8 genes) from K = 24,
-  // so two gene workgroups share a CU (measurement)
-  static constexpr int GT = (MMSBM_GENE_GT24 && K >= 24) ? 2 : 4;
-  static constexpr int NGW = 4 * GT;            // genes per workgroup
-  static constexpr int NT = 512;
-  static constexpr int KSPLIT = 8 / NXG;        // k-step parts over the 8 waves
-  // LDS row stride of the summed rows: = 20 mod 32 doubles, so the 8 (row lo, k = hi) addresses a
-  // ds_read_b64 lane group reads in x0_tiles fall on distinct banks (K2P = 400 at K = 20 put rows
-  // lo and lo + 2 on the same banks: 58 % of the gene kernel's LDS cycles were conflicts,
-  // profiles/r04d_k20_b8_pmc_summary.txt)
-  static constexpr int MSR = K2P + (20 - K2P % 32 + 32) % 32;
-  static constexpr int MS = NGW * MSR + KSPLIT * NGW * KP;  // doubles: summed rows + X parts
-  static constexpr int LDS_SP = 64 * KP;                    // s_partial's theta staging
-  static constexpr int LDS = (MS > LDS_SP ? MS : LDS_SP) * 8;
-  // LDS that lets two workgroups share a CU (K = 20-23): rounds of 6 partial-row entries and a
-  // 128-VGPR budget (4 waves per SIMD); above, LDS allows one workgroup and 12 entries per round
-  // keep more loads in flight (profiles/r02d_fin20_ab.txt: 221 -> 216 us at K = 20 x 8)
-  static constexpr bool TWO = 2 * LDS <= 160 * 1024 && K >= 20;
-  static constexpr int RE_CAP = TWO ? 6 : 12;
-  static constexpr int WPE = TWO ? 4 : 1;
-  static constexpr int YU = 8;                  // Y entries in flight per thread
-  // partial rows of one (gene, cell) entry loaded together per fill round; rows past these are
-  // summed one dependent load at a time (4 measured the same as 2 at K=30, 1,923.6 vs 1,924.9 us,
-  // profiles/r04s_large_ab.txt, and spills at K = 24)
-  static constexpr int RW = MMSBM_GENE_RW ? MMSBM_GENE_RW : 2;
-  static_assert(NXG * KSPLIT == 8, "gene part: one (a group, k part) per wave");
-  static_assert(NGW * K <= NT, "gene part epilogue: one (gene, a) per thread");
-  static_assert(LDS <= 160 * 1024, "gene kernel LDS over budget");
-};
-
-// X0 contraction of GT gene tiles at once: each p load feeds GT MFMAs, over the k-steps [kb, ke).
-// Mg = tile 0's row of lane lo; tile t's row is Mg + 4 t MSR.  p[a][k] = p_r[a K2 + k]; addresses
-// clamped (k >= K2: M is zero there; a >= K: the column is never stored), so every load is
-// unconditional and a round's loads go out together.
-template <int K>
-__device__ __forceinline__ void x0_tiles(const double* __restrict__ Mg, const double* __restrict__ p,
-                                         int a, int hi, int kb, int ke, double (&acc)[FT<K>::GT]) {
-  using F = FT<K>;
-  // (UB k-steps per batch; two batches in flight: 4 under the 128-VGPR budget of K = 20-23)
-  constexpr int K2 = K * K, UB = F::TWO ? 4 : 8, GT = F::GT;
-  const int ac = a < K ? a : K - 1;
-  // batches of UB k-steps, double-buffered: the next batch's p loads (L2) are in flight during
-  // this batch's MFMAs (a batch past ke loads clamped addresses and is not used)
-  auto ld = [&](int ks0, double (&bv)[UB]) {
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int ks = ks0 + u < ke ? ks0 + u : ke - 1;
-      const int k = 4 * ks + hi, kc = k < K2 ? k : K2 - 1;
-      bv[u] = p[ac * K2 + kc];
-    }
-  };
-  auto mm = [&](int ks0, const double (&bv)[UB]) {
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const bool ok = ks0 + u < ke;
-      const int k = 4 * (ok ? ks0 + u : kb) + hi;
-#pragma unroll
-      for (int t = 0; t < GT; ++t) {
-        const double m = Mg[t * 4 * F::MSR + k];
-        acc[t] = mfma4(ok ? m : 0.0, bv[u], acc[t]);
-      }
-    }
-  };
-  if (kb >= ke) return;
-  double bA[UB], bB[UB];
-  ld(kb, bA);
-#pragma unroll 1
-  for (int ks0 = kb; ks0 < ke; ks0 += 2 * UB) {
-    ld(ks0 + UB, bB);
-    mm(ks0, bA);
-    ld(ks0 + 2 * UB, bA);
-    if (ks0 + UB < ke) mm(ks0 + UB, bB);
-  }
-}
-
-// Gene part: 16 genes per workgroup (4 MFMA row tiles), 8 waves.  For each rating in order, the
-// 16 genes' stream-0 partial rows are summed into LDS; wave w then takes a group w % NXG and k-step
-// part w / NXG of all 4 gene tiles.  The k parts are added in order in the epilogue.
-template <int K>
-__device__ __forceinline__ void genes_x0(const double* __restrict__ pr, const double* __restrict__ prows,
-                                         const int* __restrict__ prow_ptr, int P, int R,
-                                         long long n_prows, double* __restrict__ x0, double* Ms,
-                                         int gw, Stamp& st_) {
-  using F = FT<K>;
-  constexpr int K2 = F::K2, K3 = K * K * K, NGW = F::NGW, NT = F::NT, KP = F::KP;
-  const int tid = threadIdx.x, b = blockIdx.y;
-  const int lane = tid & 63, wv = tid >> 6;
-  const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
-  const int g0 = gw * NGW;
-  const double* __restrict__ pb = prows + (size_t)b * n_prows * K2;
-  double* Xr = Ms + NGW * F::MSR;  // [KSPLIT][NGW][KP]
-  __shared__ int pp[MAX_R][NGW + 1];
-  {
-    const int c = tid / (NGW + 1), i = tid % (NGW + 1);
-    const int v = prow_ptr[(size_t)(c < R ? c : 0) * (P + 1) + (g0 + i < P ? g0 + i : P)];
-    if (c < R) pp[c][i] = v;
-  }
-  const int xg = wv % F::NXG, ksp = wv / F::NXG;
-  const int kb = F::KS * ksp / F::KSPLIT, ke = F::KS * (ksp + 1) / F::KSPLIT;
-  const int a = 4 * (4 * xg + blk) + lo;
-  double acc[F::GT];
-#pragma unroll
-  for (int t = 0; t < F::GT; ++t) acc[t] = 0.0;
-  constexpr int NE = NGW * F::K2P;
-  constexpr int NEPT = (NE + NT - 1) / NT, RE = NEPT < F::RE_CAP ? NEPT : F::RE_CAP;
-  // one round of RE entries per thread: each entry's first two partial rows loaded with the whole
-  // round in flight (addresses clamped, loads unconditional); the first round of the next rating
-  // is loaded before this rating's contraction, so its latency hides under the MFMAs.  Only the
-  // loaded values stay live; ranges are re-read from LDS when the round is stored.
-  constexpr int RW = F::RW;
-  double vr[RW][RE];
-  auto entry = [&](int r, int idx, int& qa, int& qb, int& kk) {
-    const int gl = idx / F::K2P, k = idx % F::K2P;
-    const bool ok = idx < NE && k < K2;
-    qa = ok ? pp[r][gl] : 0;
-    qb = ok ? pp[r][gl + 1] : 0;
-    kk = k < K2 ? k : 0;
-  };
-  auto load_round = [&](int r, int i0) {
-#pragma unroll
-    for (int u = 0; u < RE; ++u) {
-      int qa, qb, kk;
-      entry(r, i0 + u * NT, qa, qb, kk);
-#pragma unroll
-      for (int j = 0; j < RW; ++j) vr[j][u] = pb[(size_t)(qa + j < qb ? qa + j : 0) * K2 + kk];
-    }
-  };
-  auto store_round = [&](int r, int i0) {
-#pragma unroll
-    for (int u = 0; u < RE; ++u) {
-      const int idx = i0 + u * NT;
-      int qa, qb, kk;
-      entry(r, idx, qa, qb, kk);
-      double m = qa < qb ? vr[0][u] : 0.0;  // rows in order
-#pragma unroll
-      for (int j = 1; j < RW; ++j)
-        if (qa + j < qb) m += vr[j][u];
-      for (int q = qa + RW; q < qb; ++q) m += pb[(size_t)q * K2 + kk];
-      if (idx < NE) Ms[(idx / F::K2P) * F::MSR + idx % F::K2P] = m;
-    }
-  };
-  __syncthreads();  // pp
-  // ratings whose 16 genes have no stream-0 partial row contribute zero: skipped (uniform)
-  auto live = [&](int r) { return pp[r][0] < pp[r][NGW]; };
-  int rn = 0;
-  while (rn < R && !live(rn)) ++rn;
-  if (rn < R) load_round(rn, tid);
-  for (int r = rn; r < R;) {
-    int nxt = r + 1;
-    while (nxt < R && !live(nxt)) ++nxt;
-    __syncthreads();  // the previous rating's contraction is done with Ms
-    st_.mark(4);
-    store_round(r, tid);
-    for (int i0 = tid + RE * NT; i0 < NE; i0 += RE * NT) {
-      load_round(r, i0);
-      store_round(r, i0);
-    }
-    st_.mark(5);
-    __syncthreads();
-    st_.mark(1);
-    if (nxt < R) load_round(nxt, tid);
-    const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
-    x0_tiles<K>(Ms + (size_t)lo * F::MSR, p, a, hi, kb, ke, acc);
-    r = nxt;
-  }
-  st_.mark(2);
-  // X0[gene 4 t + hi][a]: the k parts added in order
-#pragma unroll
-  for (int t = 0; t < F::GT; ++t)
-    if (a < K) Xr[(ksp * NGW + 4 * t + hi) * KP + a] = acc[t];
-  __syncthreads();
-  const int eg = tid / K, ex = tid % K;
-  if (tid < NGW * K && g0 + eg < P) {
-    double X = Xr[eg * KP + ex];
-#pragma unroll
-    for (int q = 1; q < F::KSPLIT; ++q) X += Xr[(q * NGW + eg) * KP + ex];
-    x0[((size_t)b * P + g0 + eg) * K + ex] = X;
-  }
-  st_.mark(3);
-  st_.flush(2, ((long long)b * gridDim.x + gw) * 8 + wv, lane);
-}
-
-// Y part: thread (g, x) = item sums component x of gene g's Y entries [yptr[g], yptr[g + 1]) in
-// entry order, YU loads in flight (a hub gene has many entries).
-template <int K>
-__device__ __forceinline__ void genes_ysum(const double* __restrict__ yb, const int* __restrict__ yptr,
-                                           long long item, int P, double* __restrict__ ysum_b) {
-  constexpr int YU = FT<K>::YU;
-  if (item >= (long long)P * K) return;
-  const int g = (int)(item / K), x = (int)(item % K);
-  const int e0 = yptr[g], e1 = yptr[g + 1];
-  double S = 0.0;
-  for (int e = e0; e < e1; e += YU) {
-    double v[YU];
-#pragma unroll
-    for (int u = 0; u < YU; ++u) v[u] = yb[(size_t)(e + u < e1 ? e + u : e) * y_stride(K) + x];
-#pragma unroll
-    for (int u = 0; u < YU; ++u)
-      if (e + u < e1) S += v[u];
-  }
-  ysum_b[item] = S;
-}
-
-// The Y sums as a launch of their own (no LDS), on a second stream beside gene_kernel
-// (MMSBM_YSPLIT=1, measurement): HBM-bound Y sums beside the MFMA / L2-bound gene and S
-// workgroups.  Measured no faster (mmsbm_ctx::ysplit).
-template <int K>
-__global__ __launch_bounds__(256) void ysum_kernel(const double* __restrict__ ybuf, const int* __restrict__ yptr,
-                                                   double* __restrict__ ysum, int P, long long n_y) {
-  const int b = blockIdx.y;
-  const long long item = (long long)blockIdx.x * 256 + threadIdx.x;
-  genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
-}
-
-template <int K>
-__global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(FT<K>::WPE))) void gene_kernel(
-    const double* __restrict__ theta, const double* __restrict__ pr, const double* __restrict__ prows,
-    const int* __restrict__ prow_ptr, const int* __restrict__ prow_gene, const int* __restrict__ sp_desc,
-    const double* __restrict__ ybuf, const int* __restrict__ yptr, double* __restrict__ x0,
-    double* __restrict__ ysum, double* __restrict__ spart, int P, int R, long long n_prows,
-    long long n_y, int n_sp, int n_gene_wg, int n_sp_wg) {
-  using T = KT<K>;
-  extern __shared__ __attribute__((aligned(16))) double Ms[];
-  const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
-  Stamp st_{};
-  st_.mark(0);
-  // Workgroup kind and index from blockIdx (MMSBM_GENE_MIX above; the interleaved form is
-  // Bresenham: Y workgroups among all, then S among the rest).  Which kind and index a workgroup
-  // gets never changes what it computes.
-  const long long n_all = (long long)gridDim.x, m = (long long)n_gene_wg + n_sp_wg, n_yw = n_all - m;
-#if MMSBM_GENE_MIX
-  const long long ya = (long long)w * n_yw / n_all;
-  const bool is_y = (long long)(w + 1) * n_yw / n_all > ya;
-  const int j = w - (int)ya;  // index among the gene and S workgroups
-  const int sa = m ? (int)((long long)j * n_sp_wg / m) : 0;
-  const bool is_s = !is_y && m && (long long)(j + 1) * n_sp_wg / m > sa;
-#else  // measurement: gene, S, then Y workgroups in blockIdx order
-  const bool is_y = w >= m, is_s = !is_y && w >= n_gene_wg;
-  const long long ya = w - m;
-  const int j = w, sa = is_s ? w - n_gene_wg : 0;  // (j - sa: the gene workgroup index)
-#endif
-#ifdef MMSBM_GENE_ONLY  // measurement builds: run one workgroup kind only (1 gene, 2 S, 4 Y)
-  {
-    const int kind = is_y ? 4 : is_s ? 2 : 1;
-    if (!(MMSBM_GENE_ONLY & kind)) return;
-  }
-#endif
-  if (!is_y && !is_s) {
-    genes_x0<K>(pr, prows, prow_ptr, P, R, n_prows, x0, Ms, j - sa, st_);
-  } else if (is_s) {
-    const int lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
-    const int sw = sa, sp = sw / T::NIG, ig = sw % T::NIG;
-    const int* d = sp_desc + 3 * sp;
-    s_partial<K, FT<K>::TWO ? 4 : 8>(theta + (size_t)b * P * K, prows + (size_t)b * n_prows * T::K2, prow_gene,
-                                     d[1], d[2], spart + ((size_t)b * n_sp + sp) * T::K3, Ms, ig, tid, wv, hi,
-                                     blk, lo, st_);
-    st_.flush(3, ((long long)b * gridDim.x + w) * NW + wv, lane);
-  } else {
-    const long long item = ya * FT<K>::NT + tid;
-    genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
-  }
-}
-
-// The S and Y workgroups as a launch of their own, after the gene (x0) workgroups' launch
-// (mmsbm_ctx::gsplit): they need 16 KB of LDS (s_partial's theta staging) or none, and at most
-// 128 VGPRs, so four of them share a CU, where inside gene_kernel they inherit its LDS (150 KB at
-// K = 30) and VGPR budget and run one per CU.
-template <int K>
-__global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(4))) void gene_sy_kernel(
-    const double* __restrict__ theta, const double* __restrict__ prows, const int* __restrict__ prow_gene,
-    const int* __restrict__ sp_desc, const double* __restrict__ ybuf, const int* __restrict__ yptr,
-    double* __restrict__ ysum, double* __restrict__ spart, int P, long long n_prows, long long n_y, int n_sp,
-    int n_sp_wg) {
-  using T = KT<K>;
-  extern __shared__ __attribute__((aligned(16))) double Ms[];
-  const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
-  Stamp st_{};
-  if (w < n_sp_wg) {
-    const int lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int hi = lane >> 4, blk = (lane >> 2) & 3, lo = lane & 3;
-    const int sp = w / T::NIG, ig = w % T::NIG;
-    const int* d = sp_desc + 3 * sp;
-    s_partial<K, 8>(theta + (size_t)b * P * K, prows + (size_t)b * n_prows * T::K2, prow_gene, d[1], d[2],
-                    spart + ((size_t)b * n_sp + sp) * T::K3, Ms, ig, tid, wv, hi, blk, lo, st_);
-  } else {
-    const long long item = (long long)(w - n_sp_wg) * FT<K>::NT + tid;
-    genes_ysum<K>(ybuf + (size_t)b * (n_y + 1) * y_stride(K), yptr, item, P, ysum + (size_t)b * P * K);
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // gm_kernel (round 5; launch 2 of a large-K iteration): both contractions of the stream-0 partial
@@ -1177,9 +774,6 @@ __global__ __launch_bounds__(FT<K>::NT) __attribute__((amdgpu_waves_per_eu(4))) 
 // workgroups (16 genes each, all of p_r re-read from L2 per workgroup) and gene_sy's S workgroups
 // (a second read of every partial row).
 // ------------------------------------------------------------------------------------------
-#ifndef MMSBM_GM
-#define MMSBM_GM 1
-#endif
 // gm_kernel occupancy hint: 4 waves per SIMD (<= 128 VGPRs, two 72 KB workgroups per CU) where
 // that does not spill (K <= 16); above, the S accumulators and staging take up to 254 VGPRs and the
 // hint is free (one workgroup per CU; 128 spilled 58-120 VGPRs at K = 20-32)
@@ -1190,8 +784,12 @@ struct GM {
   static constexpr int AP = 16 * NA;
   static constexpr int RT = 64, CW = 64;     // rows per row tile, cells per chunk
   static constexpr int NCH = (K2 + CW - 1) / CW;
-  static constexpr int CS = NCH > 8 ? 2 : 1;              // cell groups (workgroups) per part
-  static constexpr int CPG = (NCH + CS - 1) / CS;         // chunks per group
+  // X rows in two halves of the chunks, [0, HALF) and [HALF, NCH), whatever the launch (round 6):
+  // a part's cells run as one workgroup (CS = 1, both halves in one) or two (CS = 2, one half
+  // each) with the same bits, so the launch can choose CS per batch (upd adds the halves in order)
+  static constexpr int HALF = (NCH + 1) / 2;
+  static constexpr int NH = NCH > 1 ? 2 : 1;               // X-row halves
+  static constexpr bool ONE = NCH <= 8;                   // CS = 1 possible (its S accumulators fit)
   static constexpr int TST = AP == 32 ? 48 : 16;  // theta tile row stride (= 16 mod 32 doubles)
   static constexpr int XT = 4 * NA, XK = 8 / XT;  // X tiles per row tile, k-splits per tile
   static constexpr int ST = 4 * NA, SK = 8 / ST;  // S tiles per chunk, row splits per tile
@@ -1208,7 +806,7 @@ struct GM {
 // column swizzle of the 64-wide LDS tiles: bit 4 <- row bit 0, bits 1-3 <- row bits 1-3
 __device__ __forceinline__ int gm_swz(int r) { return ((r & 1) << 4) | (((r >> 1) & 7) << 1); }
 
-template <int K>
+template <int K, int CS>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE))) void gm_kernel(const double* __restrict__ theta, const double* __restrict__ pr,
                                                   const double* __restrict__ prows,
                                                   const int* __restrict__ prow_gene,
@@ -1223,23 +821,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
   double* Tl = Pt + AP * CW;         // [RT][TST]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int w = blockIdx.x / G::CS, grp = blockIdx.x % G::CS, b = blockIdx.y;
-  const int cb = grp * G::CPG;       // the group's first chunk
+  constexpr int CPG = CS == 2 ? G::HALF : G::NCH;  // chunks of this workgroup's group
+  constexpr int NXH = CS == 2 ? 1 : G::NH;          // X halves this workgroup forms
+  const int w = blockIdx.x / CS, grp = blockIdx.x % CS, b = blockIdx.y;
+  const int cb = grp * G::HALF;      // the group's first chunk (0 for CS = 1)
   const int l15 = lane & 15, l4 = lane >> 4;
   const int* d = sp_desc + 3 * w;
   const int r = d[0], q0 = d[1], q1 = d[2];
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
   const double* __restrict__ mb = prows + (size_t)b * n_prows * K2;
-  double* __restrict__ xb = xrow + (size_t)grp * xgs + (size_t)b * n_prows * K;  // xgs: a group's X rows
+  double* __restrict__ xb = xrow + (size_t)grp * xgs + (size_t)b * n_prows * K;  // xgs: one half's X rows
   // this wave's X tile (row tile xr, a tile xa, k-split xk) and S tile (cell tile sc, a tile sa,
   // row split sk) of every chunk
   const int xt = wv % G::XT, xk = wv / G::XT, xr = xt % 4, xa = xt / 4;
   const int st = wv % G::ST, sk = wv / G::ST, sc = st % 4, sa = st / 4;
   constexpr int XKS = 16 / G::XK, SKS = 16 / G::SK;  // k-steps per split
-  d4v sacc[G::CPG];
+  d4v sacc[CPG];
 #pragma unroll
-  for (int c = 0; c < G::CPG; ++c) sacc[c] = d4v{0.0, 0.0, 0.0, 0.0};
+  for (int c = 0; c < CPG; ++c) sacc[c] = d4v{0.0, 0.0, 0.0, 0.0};
   typedef double d2v __attribute__((ext_vector_type(2)));
   using MV = typename std::conditional<G::MW == 2, d2v, double>::type;
 
@@ -1311,9 +911,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
     load_p(cb, pv);
   }
   for (int qt = q0; qt < q1; qt += RT) {
-    d4v xacc = d4v{0.0, 0.0, 0.0, 0.0};
+    d4v xacc[NXH];
 #pragma unroll
-    for (int i = 0; i < G::CPG; ++i) {
+    for (int j = 0; j < NXH; ++j) xacc[j] = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < CPG; ++i) {
       const int c = cb + i;
       if (c >= G::NCH) break;  // (uniform: the last group may hold fewer chunks)
       __syncthreads();  // the previous chunk's reads of the LDS tiles are done
@@ -1321,7 +923,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
       if (i == 0) store_t(tv);
       __syncthreads();
       // next chunk (or the next row tile's first chunk and theta rows) in flight
-      if (i + 1 < G::CPG && c + 1 < G::NCH) {
+      if (i + 1 < CPG && c + 1 < G::NCH) {
         load_m(qt, c + 1, mv);
         load_p(c + 1, pv);
       } else if (qt + RT < q1) {
@@ -1329,11 +931,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
         load_p(cb, pv);
         load_t(qt + RT, tv);
       }
-      // X tile: rows 16 xr + i, a 16 xa + j; k = the chunk's cells
+      // X tile: rows 16 xr + i, a 16 xa + j; k = the chunk's cells, into the chunk's half
+      const int hx = (CS == 2 || i < G::HALF) ? 0 : 1;  // (compile-time: i is unrolled, cb = 0 for CS = 1)
 #pragma unroll 4
       for (int s = xk * XKS; s < (xk + 1) * XKS; ++s) {
         const int cell = 4 * s + l4;
-        xacc = mfma16(xm[cell ^ xsw_m], xp[cell ^ xsw_p], xacc);
+        xacc[hx] = mfma16(xm[cell ^ xsw_m], xp[cell ^ xsw_p], xacc[hx]);
       }
       // S tile: a 16 sa + i, cells 16 sc + j of the chunk; k = the tile's rows
 #pragma unroll 4
@@ -1342,33 +945,39 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
         sacc[i] = mfma16(sT[row * TST], Ml[row * CW + (scell ^ gm_swz(row))], sacc[i]);
       }
     }
-    // X rows of this tile: the k-splits' parts added in wave order (XK = 2: through LDS)
+    // X rows of this tile, per half: the k-splits' parts added in wave order (XK = 2: through LDS)
     if constexpr (G::XK == 1) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = 16 * xr + l4 + 4 * i, a = 16 * xa + l15;
-        if (qt + row < q1 && a < K) xb[(size_t)(qt + row) * K + a] = xacc[i];
-      }
-    } else {
-      __syncthreads();  // Ml is free: park split 1's parts there
-      if (xk == 1)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Ml[(xt * 4 + i) * 64 + lane] = xacc[i];
-      __syncthreads();
-      if (xk == 0)
+      for (int j = 0; j < NXH; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = 16 * xr + l4 + 4 * i, a = 16 * xa + l15;
-          const double v = xacc[i] + Ml[(xt * 4 + i) * 64 + lane];
-          if (qt + row < q1 && a < K) xb[(size_t)(qt + row) * K + a] = v;
+          if (qt + row < q1 && a < K) xb[j * xgs + (size_t)(qt + row) * K + a] = xacc[j][i];
         }
+    } else {
+      __syncthreads();  // Ml is free: park split 1's parts there (half j at 2048 j)
+      if (xk == 1)
+#pragma unroll
+        for (int j = 0; j < NXH; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) Ml[2048 * j + (xt * 4 + i) * 64 + lane] = xacc[j][i];
+      __syncthreads();
+      if (xk == 0)
+#pragma unroll
+        for (int j = 0; j < NXH; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = 16 * xr + l4 + 4 * i, a = 16 * xa + l15;
+            const double v = xacc[j][i] + Ml[2048 * j + (xt * 4 + i) * 64 + lane];
+            if (qt + row < q1 && a < K) xb[j * xgs + (size_t)(qt + row) * K + a] = v;
+          }
     }
   }
   // the part's S partial over the group's cells: the row splits' parts added in wave order
   double* __restrict__ out = spart + ((size_t)b * n_sp + w) * K3;
   if constexpr (G::SK == 2) __syncthreads();
 #pragma unroll
-  for (int i = 0; i < G::CPG; ++i) {
+  for (int i = 0; i < CPG; ++i) {
     const int c = cb + i;
     if (c >= G::NCH) break;
     if constexpr (G::SK == 2) {
@@ -1393,7 +1002,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
 
 // ------------------------------------------------------------------------------------------
 // upd_kernel (launch 3), grid (theta workgroups + cell workgroups + q workgroups, B), block 512:
-//   theta workgroups: thread (g, a): X = x0 + ysum (+ the joint model's pair sums);
+//   theta workgroups: one wave per gene, lane a: X = the gene's gm_kernel X rows + its Y entries
+//     (+ the joint model's pair sums);
 //     theta' = theta X / deg (:1016-1018), or SUMS: nth = X
 //   cell workgroups: 64 cells x 8 parts; S_r = sum of the rating's S partials (fixed order);
 //     p' = p S / (eps + sum_r p S) in place (:1021-1028), or SUMS: S_out = S
@@ -1403,8 +1013,8 @@ constexpr int UPD_NT = 512;
 
 template <int K, bool SUMS>
 __global__ __launch_bounds__(UPD_NT) void upd_kernel(
-    double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ x0,
-    const double* __restrict__ ysum, const double* __restrict__ spart, const int* __restrict__ deg,
+    double* __restrict__ theta, double* __restrict__ pr, const double* __restrict__ spart,
+    const int* __restrict__ deg,
     SpRange spr, int P, int R, int n_sp, int n_th_wg, double eps, double* __restrict__ nth_out,
     double* __restrict__ S_out, const double* __restrict__ nth_add, const double* __restrict__ q_part,
     double* __restrict__ q_out, int n_qwg, const double* __restrict__ xrow, const int* __restrict__ prow_ptr,
@@ -1415,44 +1025,63 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
   __shared__ double red[MAX_R * NPART * 64];
   const int tid = threadIdx.x, b = blockIdx.y, w = blockIdx.x;
   if (w < n_th_wg) {
-    const long long item = (long long)w * UPD_NT + tid;
-    if (item >= (long long)P * K) return;  // no barrier in this branch
-    const size_t o = (size_t)b * P * K + item;
-    double X;
-    if (xrow) {  // gm_kernel: the gene's X rows, rating then row order, cell groups in order
-      const int g = (int)(item / K), a = (int)(item % K);
-      const double* __restrict__ xb = xrow + (size_t)b * n_prows * K + a;
-      X = 0.0;
-      for (int r = 0; r < R; ++r)
-        for (int q = prow_ptr[(size_t)r * (P + 1) + g], qe = prow_ptr[(size_t)r * (P + 1) + g + 1]; q < qe; ++q) {
-          double x = xb[(size_t)q * K];
+    // one wave per gene (round 6): its X rows (lanes a < K), then its Y entries with 16-byte loads
+    // over the whole wave (the wide coalesced form; a gene's entries are one contiguous block and
+    // YS is a multiple of 4 doubles): lane l < LW reads words 2 l, 2 l + 1 of each WW-word step,
+    // components 2 l mod YS and 2 l + 1 mod YS (WW = EPI YS, whole entries; pad components are
+    // summed apart and never used), YU2 steps in flight; the lanes of one component are then
+    // added in order through LDS
+    const int lane = tid & 63, wv = tid >> 6;
+    const int g = w * (UPD_NT / 64) + wv;
+    if (g >= P) return;  // (wave-uniform; no barrier in this branch)
+    const int a = lane < K ? lane : 0;
+    const size_t o = ((size_t)b * P + g) * K + a;
+    const double th = theta[o];
+    const int dg = deg[g];
+    const double ad = nth_add ? nth_add[o] : 0.0;
+    // the gene's X rows (gm_kernel), rating then row order, cell groups in order
+    const double* __restrict__ xb = xrow + (size_t)b * n_prows * K + a;
+    double X = 0.0;
+    for (int r = 0; r < R; ++r)
+      for (int q = prow_ptr[(size_t)r * (P + 1) + g], qe = prow_ptr[(size_t)r * (P + 1) + g + 1]; q < qe; ++q) {
+        double x = xb[(size_t)q * K];
 #pragma unroll
-          for (int h = 1; h < GM<K>::CS; ++h) x += xb[h * xgs + (size_t)q * K];
-          X += x;
-        }
-      if (ybuf) {  // the gene's Y entries, summed here (no ysum launch): entry order, 8 loads in flight
-        constexpr int YU = FT<K>::YU, YS = y_stride(K);
-        const double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * YS + a;
-        const int e0 = yptr[g], e1 = yptr[g + 1];
-        double Y = 0.0;
-        for (int e = e0; e < e1; e += YU) {
-          double v[YU];
-#pragma unroll
-          for (int u = 0; u < YU; ++u) v[u] = yb[(size_t)(e + u < e1 ? e + u : e) * YS];
-#pragma unroll
-          for (int u = 0; u < YU; ++u)
-            if (e + u < e1) Y += v[u];
-        }
-        X += Y;
-      } else {
-        X += ysum[o];
+        for (int h = 1; h < GM<K>::NH; ++h) x += xb[h * xgs + (size_t)q * K];
+        X += x;
       }
-    } else {
-      X = x0[o] + ysum[o];
+    constexpr int YS = y_stride(K), EPI = 128 / YS, WW = EPI * YS, LW = WW / 2, YU2 = 8;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * YS;
+    const long long w0 = (long long)yptr[g] * YS, w1 = (long long)yptr[g + 1] * YS;
+    const long long wf = w0 + 2 * (lane < LW ? lane : 0);
+    double Sa = 0.0, Sb = 0.0;
+    if (lane < LW) {
+      for (long long wd = wf; wd < w1; wd += (long long)YU2 * WW) {
+        d2 v[YU2];
+#pragma unroll
+        for (int u = 0; u < YU2; ++u)
+          v[u] = *reinterpret_cast<const d2*>(yb + (wd + (long long)u * WW < w1 ? wd + (long long)u * WW : wf));
+#pragma unroll
+        for (int u = 0; u < YU2; ++u)
+          if (wd + (long long)u * WW < w1) {
+            Sa += v[u].x;
+            Sb += v[u].y;
+          }
+      }
     }
-    if (nth_add) X += nth_add[o];
-    if constexpr (SUMS) nth_out[o] = X;
-    else theta[o] = theta[o] * X / (double)deg[item / K];
+    double* __restrict__ yr = red + wv * 128;
+    yr[2 * lane] = Sa;
+    yr[2 * lane + 1] = Sb;
+    wave_lds_sync();
+    if (lane < K) {
+      double Y = yr[lane];
+#pragma unroll
+      for (int jj = 1; jj < EPI; ++jj) Y += yr[lane + jj * YS];
+      X += Y;
+      if (nth_add) X += ad;
+      if constexpr (SUMS) nth_out[o] = X;
+      else theta[o] = th * X / (double)dg;
+    }
     return;
   }
   const int cl = tid & 63, part = tid >> 6;
@@ -1686,6 +1315,7 @@ struct Launch {
   int gmax;
   PassFn sk_pass;  // small-K kernels (sk.h), K <= 12; nullptr above
   FinFn sk_fin;
+  int (*gm_groups)(const mmsbm_ctx*, int);  // gm_kernel's workgroups per part (gm_cs<K>)
 };
 
 }  // namespace
@@ -1709,8 +1339,8 @@ struct mmsbm_ctx {
   char* ws = nullptr;
   long long ws_bytes = 0;
   // workspace views: cbuf = small-K c / large-K Y entries, prows = small-K X / large-K M^0 partial
-  // rows, spart = S partials, gx = large-K x0 then ysum ([2][B][P][K])
-  double *cbuf = nullptr, *prows = nullptr, *spart = nullptr, *gx = nullptr, *partL = nullptr;
+  // rows, spart = S partials
+  double *cbuf = nullptr, *prows = nullptr, *spart = nullptr, *partL = nullptr;
   double *nth_tmp = nullptr, *S_tmp = nullptr;  // fin_kernel sums-out scratch (kernel timing)
   const double* nth_add = nullptr;  // joint model: pair sums added before the degree division
   const double* q_part = nullptr;   // joint model: S2 partials for fin's q cells (null = none)
@@ -1729,20 +1359,9 @@ struct mmsbm_ctx {
   bool warm = false;                 // a direct iteration ran (LDS opt-ins done before capture)
   hipStream_t cap = nullptr;         // capture stream (torch's default stream cannot be captured)
   hipGraphExec_t gexec = nullptr;
-  // large-K Y sums inside gene_kernel, or (MMSBM_YSPLIT=1, measurement) as ysum_kernel on a second
-  // stream forked from the caller's after pass A and joined before the update: no overlap gained
-  // (K=30 gene 1,930 vs 1,928 us; K=20 x 8 128 vs 113 us, profiles/r04r_ysplit_ab.txt) — the gene
-  // kernel's waves leave a CU no VGPRs for the Y waves
-  bool ysplit = false;
-  // large-K gene kernel as two launches: x0 workgroups, then S + Y workgroups (gene_sy_kernel) at
-  // their own LDS and VGPR budget; MMSBM_GSPLIT=0: one launch (measurement)
-  bool gsplit = true;
-  // large-K M-step contractions in gm_kernel (round 5); MMSBM_GM=0: round 4's gene kernel (measurement)
-  bool gm = MMSBM_GM != 0;
-  bool yupd = true;              // gm path: Y sums inside upd_kernel (MMSBM_YUPD=0: own launch)
-  double* xrows = nullptr;       // gm_kernel's X rows [B][n_prows][K]
-  hipStream_t ys = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  double* xrows = nullptr;       // gm_kernel's X rows [2 halves][B][n_prows][K]
+  int ncu = 256;                 // the device's compute units (gm_kernel's split rule)
+  int gm_cs = 0;                 // MMSBM_GM_CS: force gm_kernel's workgroups per part (0: by batch)
   const double *g_theta = nullptr, *g_pr = nullptr;
   unsigned long long g_gen = 0;
   int g_iters = 0;
@@ -1754,7 +1373,7 @@ namespace {
 inline int nb_of(const mmsbm_ctx* c) { return c->nact > 0 && c->nact < c->B ? c->nact : c->B; }
 
 struct WsLayout {
-  size_t cbuf, prows, spart, gx, partL, nth, S, xrows, total;
+  size_t cbuf, prows, spart, partL, nth, S, xrows, total;
 };
 
 WsLayout ws_layout(const mmsbm_ctx* c) {
@@ -1774,7 +1393,6 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
     off += align_up(c->sk_y ? 8 : B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
     L.spart = off;
     off += align_up(B * std::max(tr.n_wg_a, 1) * K3 * 8);
-    L.gx = off;
     L.partL = off;
     off += align_up(B * std::max({tr.n_wg_a, te.n_wg_a, 1}) * 8);
     L.nth = off;
@@ -1784,23 +1402,21 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
     L.total = off;
     return L;
   }
-  // large-K: Y entries (+ the dummy entry of padding rows), M^0 partial rows, S partials, x0 and
-  // ysum, likelihood partials, fin's sums-out scratch
+  // large-K: Y entries (+ the dummy entry of padding rows), M^0 partial rows, S partials,
+  // likelihood partials, fin's sums-out scratch, gm_kernel's X rows
   L.cbuf = off;
   off += align_up(B * (tr.n_y + 1) * y_stride(c->K) * 8);
   L.prows = off;
   off += align_up(B * std::max<long long>(tr.n_prows, 1) * K2 * 8);
   L.spart = off;
   off += align_up(B * std::max(tr.n_sp, 1) * K3 * 8);
-  L.gx = off;
-  off += align_up(2 * B * (size_t)c->P * c->K * 8);
   L.partL = off;
   off += align_up(B * std::max({tr.n_wg_a, te.n_wg_a, 1}) * 8);
   L.nth = off;
   off += align_up(B * (size_t)c->P * c->K * 8);
   L.S = off;
   off += align_up(B * c->R * K3 * 8);
-  L.xrows = off;  // gm_kernel's X rows: two cell groups at most (GM<K>::CS)
+  L.xrows = off;  // gm_kernel's X rows: two halves (GM<K>::NH)
   off += align_up(2 * B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
   L.total = off;
   return L;
@@ -1830,65 +1446,44 @@ int lds_opt_in(mmsbm_ctx* c, unsigned bit, KernelT* kern, int bytes) {
   return MMSBM_OK;
 }
 
+// gm_kernel's workgroups per part (the bits are the same either way, GM<K>::HALF): two where the
+// doubled grid still fits one round of resident workgroups (one sample at K = 13-22: the grid is a
+// few dozen parts; r05: K=20 +24 %, K=16 +13.5 %), one where it would not (K=20 x 8: -6 % with
+// two); two always where one workgroup's S accumulators would not fit (NCH > 8); one for a single
+// chunk.  MMSBM_GM_CS=1/2 forces it where both exist (tests, measurement).
+template <int K>
+int gm_cs(const mmsbm_ctx* c, int nsp) {
+  using G = GM<K>;
+  if (!G::ONE) return 2;
+  if (G::NCH == 1) return 1;
+  if (c->gm_cs == 1 || c->gm_cs == 2) return c->gm_cs;
+  const long long slots = (long long)c->ncu * (G::WPE >= 4 ? 2 : 1);
+  return 2LL * nsp * nb_of(c) <= slots ? 2 : 1;
+}
+
 template <int K>
 int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const double* pr,
                 hipStream_t s) {
   using T = KT<K>;
-  using F = FT<K>;
   const SetDev& sd = c->sets[which];
   const auto& h = sd.h;
   int rc;
-  if (mode == PASS_B) {  // launch 2: the gene kernel (x0, S partials, Y sums) of the train plan
-    const int ngw = (c->P + F::NGW - 1) / F::NGW;
-    const int nspw = std::max(h.n_sp, 1) * T::NIG;
-    const int nyw = c->ysplit ? 0 : (int)(((long long)c->P * K + F::NT - 1) / F::NT);
-    if ((rc = lds_opt_in(c, 8, &gene_kernel<K>, F::LDS))) return rc;
-    const size_t pk = (size_t)c->B * c->P * K;
-    if (c->ysplit) {  // the Y sums on the second stream, from the same point of the caller's stream
-      if (!c->ys) {
-        HIP_TRY(hipStreamCreateWithFlags(&c->ys, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+  if (mode == PASS_B) {  // launch 2: gm_kernel (X rows + S partials in one pass); upd sums Y
+    const int nsp = std::max(h.n_sp, 1);
+    if (gm_cs<K>(c, nsp) == 1) {
+      if constexpr (GM<K>::ONE) {
+        if ((rc = lds_opt_in(c, 10, &gm_kernel<K, 1>, GM<K>::LDS))) return rc;
+        gm_kernel<K, 1><<<dim3(nsp, nb_of(c)), 512, GM<K>::LDS, s>>>(
+            theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, h.n_prows, nsp,
+            (long long)c->B * h.n_prows * K);
       }
-      HIP_TRY(hipEventRecord(c->ev_fork, s));
-      HIP_TRY(hipStreamWaitEvent(c->ys, c->ev_fork, 0));
-      const long long nyb = ((long long)c->P * K + 255) / 256;
-      ysum_kernel<K><<<dim3((unsigned)nyb, nb_of(c)), 256, 0, c->ys>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
-      HIP_TRY(hipGetLastError());
-    }
-    if (c->gm) {  // round 5: gm_kernel (X rows + S partials in one pass), then the Y sums
-      if ((rc = lds_opt_in(c, 10, &gm_kernel<K>, GM<K>::LDS))) return rc;
-      gm_kernel<K><<<dim3(std::max(h.n_sp, 1) * GM<K>::CS, nb_of(c)), 512, GM<K>::LDS, s>>>(
-          theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, h.n_prows,
-          std::max(h.n_sp, 1), (long long)c->B * h.n_prows * K);
-      HIP_TRY(hipGetLastError());
-      if (!c->yupd) {  // MMSBM_YUPD=0 (measurement): the Y sums as a launch of their own
-        const long long nyb = ((long long)c->P * K + 255) / 256;
-        ysum_kernel<K><<<dim3((unsigned)nyb, nb_of(c)), 256, 0, s>>>(c->cbuf, sd.yptr, c->gx + pk, c->P, h.n_y);
-        HIP_TRY(hipGetLastError());
-      }
-      return MMSBM_OK;
-    }
-    // two launches from K = 24 (K=30 gene 1,778 -> 1,745 us, profiles/r04w_gsplit_ab.txt); at
-    // K = 20-23 two gene workgroups share a CU and the single launch, whose S and Y workgroups
-    // overlap the x0 ones, is faster (K=20 x 8: 129.5 vs 154.7 us, profiles/r04v_gsplit_ab.txt)
-    if (c->gsplit && K >= 24) {  // x0 workgroups, then the S and Y workgroups at their own budget
-      gene_kernel<K><<<dim3(ngw, nb_of(c)), F::NT, F::LDS, s>>>(
-          theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
-          c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, 0);
-      HIP_TRY(hipGetLastError());
-      gene_sy_kernel<K><<<dim3(nspw + nyw, nb_of(c)), F::NT, F::LDS_SP * 8, s>>>(
-          theta, c->prows, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx + pk, c->spart, c->P, h.n_prows,
-          h.n_y, std::max(h.n_sp, 1), nspw);
     } else {
-      gene_kernel<K><<<dim3(ngw + nspw + nyw, nb_of(c)), F::NT, F::LDS, s>>>(
-          theta, pr, c->prows, sd.prow_ptr, sd.prow_gene, sd.sp_desc, c->cbuf, sd.yptr, c->gx, c->gx + pk,
-          c->spart, c->P, c->R, h.n_prows, h.n_y, std::max(h.n_sp, 1), ngw, nspw);
-    }
-    if (c->ysplit) {
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipEventRecord(c->ev_join, c->ys));
-      HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+      if constexpr (GM<K>::NCH > 1) {
+        if ((rc = lds_opt_in(c, 11, &gm_kernel<K, 2>, GM<K>::LDS))) return rc;
+        gm_kernel<K, 2><<<dim3(2 * nsp, nb_of(c)), 512, GM<K>::LDS, s>>>(
+            theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, h.n_prows, nsp,
+            (long long)c->B * h.n_prows * K);
+      }
     }
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
@@ -1911,34 +1506,32 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
   return MMSBM_OK;
 }
 
-// launch 3: upd_kernel (theta from x0 + ysum, p from the S partials; sums-out mode for the
+// launch 3: upd_kernel (theta from the X rows + Y entries, p from the S partials; sums-out mode for the
 // link-sharded accumulate and kernel timing)
 template <int K>
 int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, double* S,
                hipStream_t s) {
   const SetDev& sd = c->sets[MMSBM_SET_TRAIN];
   const auto& h = sd.h;
-  const int nthw = (int)(((long long)c->P * K + UPD_NT - 1) / UPD_NT);
+  const int nthw = (c->P + UPD_NT / 64 - 1) / (UPD_NT / 64);  // one wave per gene
   const int ncw = (K * K * K + 63) / 64;
   SpRange spr{};
   for (int r = 0; r < c->R; ++r) {
     spr.lo[r] = h.sp_lo[r];
     spr.hi[r] = h.sp_hi[r];
   }
-  const size_t pk = (size_t)c->B * c->P * K;
   // joint model: the q cells (qr M-step from the pair launch's S2 partials), theta update only
   const int nqc = (!sums && c->q_part) ? (K * K + 63) / 64 : 0;
-  const double* xr = c->gm ? c->xrows : nullptr;  // gm_kernel's X rows, or gene_kernel's x0
-  // gm path: the theta workgroups sum each gene's Y entries themselves (round 5)
-  const double* yb = (c->gm && c->yupd) ? c->cbuf : nullptr;
+  const double* xr = c->xrows;  // gm_kernel's X rows; the theta workgroups sum the Y entries (cbuf)
+  const double* yb = c->cbuf;
   if (sums)
     upd_kernel<K, true><<<dim3(nthw + ncw, nb_of(c)), UPD_NT, 0, s>>>(
-        theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
+        theta, pr, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
         nth, S, c->nth_add, nullptr, nullptr, 0, xr, sd.prow_ptr, h.n_prows, (long long)c->B * h.n_prows * K,
         yb, sd.yptr, h.n_y);
   else
     upd_kernel<K, false><<<dim3(nthw + ncw + nqc, nb_of(c)), UPD_NT, 0, s>>>(
-        theta, pr, c->gx, c->gx + pk, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
+        theta, pr, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
         nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg, xr, sd.prow_ptr, h.n_prows,
         (long long)c->B * h.n_prows * K, yb, sd.yptr, h.n_y);
   HIP_TRY(hipGetLastError());
@@ -2056,7 +1649,7 @@ constexpr auto make_table(std::integer_sequence<int, Ks...>) {
   return std::array<Launch, sizeof...(Ks)>{Launch{&launch_pass<Ks + 1>, &launch_fin<Ks + 1>,
                                                   &launch_mapply<Ks + 1>, &launch_predict<Ks + 1>,
                                                   KT<Ks + 1>::GMAX, sk_pass_fn<Ks + 1>(),
-                                                  sk_fin_fn<Ks + 1>()}...};
+                                                  sk_fin_fn<Ks + 1>(), &gm_cs<Ks + 1>}...};
 }
 
 
@@ -2165,10 +1758,12 @@ int mmsbm_create(int device, mmsbm_ctx** out) {
   auto* c = new mmsbm_ctx();
   c->device = device;
   if (const char* gi = getenv("MMSBM_GRAPH")) c->graph_iters = std::max(0, atoi(gi));
-  if (const char* ysp = getenv("MMSBM_YSPLIT")) c->ysplit = ysp[0] != '0';
-  if (const char* gsp = getenv("MMSBM_GSPLIT")) c->gsplit = gsp[0] != '0';
-  if (const char* gme = getenv("MMSBM_GM")) c->gm = gme[0] != '0';
-  if (const char* yu = getenv("MMSBM_YUPD")) c->yupd = yu[0] != '0';
+  if (const char* gc = getenv("MMSBM_GM_CS")) c->gm_cs = atoi(gc);
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+      c->ncu = ncu;
+  }
   if (MMSBM_STAMP && getenv("MMSBM_STAMP")) {
     DeviceGuard g(device);
     const size_t bytes = sizeof(unsigned long long) * 5 * STAMP_WAVES * STAMP_SLOTS;
@@ -2188,9 +1783,6 @@ int mmsbm_destroy(mmsbm_ctx* c) {
   if (c->stamp) (void)hipFree(c->stamp);
   if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
   if (c->cap) (void)hipStreamDestroy(c->cap);
-  if (c->ys) (void)hipStreamDestroy(c->ys);
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (auto& v : c->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   delete c;
@@ -2316,10 +1908,12 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   const bool merge = !c->sk && c->K >= MMSBM_LDS_BIG && !(mg && mg[0] == '0');
   // stream-0 partial rows per S partial at large K (each S partial is K^3 words the update sums);
   // MMSBM_SP_ROWS=n overrides it (measurement)
-  // gm_kernel (round 5): 128 rows (two 64-row tiles) per part and no cap on the parts
-  int sp_rows = c->K <= 12 ? 16 : c->gm ? 128 : 4 * c->K;
+  // gm_kernel (round 5): 128 rows (two 64-row tiles) per part, at most 1,024 parts per rating
+  // (longer parts beyond that: gm_kernel walks any number of 64-row tiles), so the S partials take
+  // at most R x 1,024 x K^3 doubles per sample whatever E (2 x 1,024 x 27,000 x 8 B = 442 MB at K=30)
+  int sp_rows = c->K <= 12 ? 16 : 128;
   if (const char* e = getenv("MMSBM_SP_ROWS")) sp_rows = std::max(4, atoi(e));
-  const int sp_cap = (!c->sk && c->gm) ? (1 << 30) : 256;
+  const int sp_cap = c->sk ? 256 : 1024;
   sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
                            c->gcap, sp_rows, c->sk, 1024, c->sk_fused,
                            mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge, sp_cap, pnw_host(c->K));
@@ -2396,7 +1990,6 @@ int mmsbm_set_workspace(mmsbm_ctx* c, void* ws, int64_t bytes) {
   c->cbuf = (double*)(c->ws + L.cbuf);
   c->prows = (double*)(c->ws + L.prows);
   c->spart = (double*)(c->ws + L.spart);
-  c->gx = (double*)(c->ws + L.gx);
   c->partL = (double*)(c->ws + L.partL);
   c->nth_tmp = (double*)(c->ws + L.nth);
   c->S_tmp = (double*)(c->ws + L.S);
@@ -2404,7 +1997,7 @@ int mmsbm_set_workspace(mmsbm_ctx* c, void* ws, int64_t bytes) {
   // small-K: the c vector's last slot (stream-1/2 padding rows read it) and the S partials stay
   // zero; large-K: Y and the S partials start zeroed (every word read is written each iteration)
   HIP_TRY(hipMemset(c->ws + L.cbuf, 0, L.prows - L.cbuf));
-  HIP_TRY(hipMemset(c->ws + L.spart, 0, L.gx - L.spart));
+  HIP_TRY(hipMemset(c->ws + L.spart, 0, L.partL - L.spart));
   HIP_TRY(hipDeviceSynchronize());
   return MMSBM_OK;
 }
@@ -2670,7 +2263,7 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[12] = c->sets[which].ncu;
   info[13] = c->sets[which].unit_target;
   info[14] = h.n_y;
-  info[15] = 0;
+  info[15] = h.small ? 0 : kTable[c->K - 1].gm_groups(c, std::max(h.n_sp, 1));
   return MMSBM_OK;
 }
 

@@ -44,6 +44,10 @@ enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
 #ifndef MMSBM_SK_PVS
 #define MMSBM_SK_PVS 1  // P^s rows at an odd stride (0: K^2, round 3), see SKT::PVS
 #endif
+#ifndef MMSBM_SK_Z16
+#define MMSBM_SK_Z16 0  // 1: SK_U's Z of four chunks per v_mfma_f64_16x16x4f64, no LDS in the chunk loop
+                        // (round 6, measured slower: fused 19.9 vs 17.3 us, profiles/r06b_z16_ab.txt)
+#endif
 #ifndef MMSBM_SK_GHOIST
 #define MMSBM_SK_GHOIST 0  // 1: the first block's theta gathers before the V tables (after the barrier)
 #endif
@@ -117,6 +121,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     double eps, const int4* __restrict__ urec1, const int* __restrict__ udesc1, int L1) {
   using T = SKT<K>;
   constexpr int NG = T::NG, K2 = T::K2, K3 = T::K3, NCT = T::NCT, NCG = T::NCG, SLOT = T::SLOT;
+  constexpr bool Z16 = MODE == SK_U && MMSBM_SK_Z16;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -338,6 +343,87 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
       }
       if (nb > LC) load_block(b0 / LC + 1, bk);  // the next block's records, in flight meanwhile
       if (!MMSBM_SK_GHOIST || b0 > 0) gather(nb);
+      if constexpr (Z16) {
+        // ---- Z of four chunks at once on v_mfma_f64_16x16x4f64, no LDS in the chunk loop (round 6).
+        // m = the 16 observations of chunks 4 g .. 4 g + 3 (record 16 g + m), k = h, n = b:
+        //   A[m][k] = theta_v(record 16 g + m)[4 hs + k]: gathered straight into lane (k = hi, m = col)
+        //   B[k][n] = V_vt[b = n][h = 4 hs + k] = vb[hs] (lane (hi, col), as the 4x4x4 path)
+        //   D[m = hi + 4 i][n = col] in element i = Z of (chunk 4 g + i, obs hi)[b = col]
+        // so lane (hi, col) holds the Z row of observation hi of each chunk in the layout of ga: d is
+        // the DPP row sum of ga * Z, c = n / d in the 16 lanes of the observation (the layout the M
+        // MFMA takes its c from), and no transpose, fence or d / c word goes through LDS.  A group
+        // crossing a stretch end takes the Z of each stretch for the chunks of that stretch.
+        // (A rows past the unit's end read a valid record: load_block clamps; they are not used.)
+        constexpr int NGR = LC / 4;
+        double za[NGR][NG];
+        auto load_za = [&](int g) {
+          if (4 * g < nb) {  // (uniform)
+            const int vg = rec[16 * g + col].y;
+            const char* __restrict__ thb = reinterpret_cast<const char*>(th);
+#pragma unroll
+            for (int hs = 0; hs < NG; ++hs) {  // (h >= K: a finite word against the zero B rows)
+              const unsigned hc = (unsigned)(4 * hs + hi < K ? 4 * hs + hi : K - 1) * 8u;
+              za[g][hs] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)vg, K * 8u) + hc));
+            }
+          } else {
+#pragma unroll
+            for (int hs = 0; hs < NG; ++hs) za[g][hs] = 0.0;
+          }
+        };
+        load_za(0);  // (then one group ahead: two groups' operands live, not four)
+        auto zmm = [&](int g) {
+          d4v D = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int hs = 0; hs < NG; ++hs) D = mfma16(za[g][hs], vb[hs], D);
+          return D;
+        };
+#pragma unroll
+        for (int g = 0; g < NGR; ++g) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (g + 1 < NGR) load_za(g + 1);
+          if (4 * g < nb) {  // (uniform)
+            const int clo = b0 + 4 * g, chi = b0 + 4 * g + (nb - 4 * g < 4 ? nb - 4 * g : 4);
+            d4v Z = zmm(g);
+            while (vsend < chi) {  // (uniform) a stretch ends inside the group: the next one's V
+              const int vstart = vsend;
+              ++vt;
+              vsend = stretch_end(vt);
+              load_v(vt);
+              const d4v Zn = zmm(g);
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                if (clo + i >= vstart) Z[i] = Zn[i];
+            }
+            if (vsend == chi && vt + 1 < nst) {  // the next group starts the next stretch
+              ++vt;
+              vsend = stretch_end(vt);
+              load_v(vt);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int q = 4 * g + i;
+              if (q < nb) {
+                const int n0 = __builtin_amdgcn_readlane(wlane, 4 * q), n1 = __builtin_amdgcn_readlane(wlane, 4 * q + 1);
+                const int n2 = __builtin_amdgcn_readlane(wlane, 4 * q + 2), n3 = __builtin_amdgcn_readlane(wlane, 4 * q + 3);
+                const int nq = hi == 0 ? n0 : hi == 1 ? n1 : hi == 2 ? n2 : n3;
+                const double d = row16_sum(ga[q] * Z[i]) + eps;
+                const double c = sk_div((double)nq, d);
+                m16 = mfma16(ga[q], c * gv[q], m16);
+                if (b0 + q + 1 == send) {  // stretch t done: its M row into slot t
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) {
+                    const int x = hi + 4 * j;
+                    if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[j];
+                  }
+                  m16 = d4v{0.0, 0.0, 0.0, 0.0};
+                  ++t;
+                  send = stretch_end(t);
+                }
+              }
+            }
+          }
+        }
+      } else {
       if constexpr (MODE != SK_B) {
         // ---- d of every observation of the block.  Per chunk: Z[obs hi][b = col] =
         // sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA (A = theta_v(obs lo)[4 hs + hi], the transpose
@@ -450,6 +536,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
           }
         }
       }
+      }  // (Z16)
     }
     st_.mark(2);
   }
@@ -936,7 +1023,8 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
 //     words l, l + LY, ... (component l mod K), the lanes of one component then added in lane
 //     order; lane x < K adds that to its X^0 partial rows (stream 0) and updates theta.
 //   cell part: 16 cells x 16 parts per workgroup: S_r[cell] = sum of the rating's S partials
-//     (one per stream-0 workgroup), parts combined in order; p' = p S / (eps + sum_r p S)
+//     (one per stream-0 workgroup), parts combined in order (every rating's loads in one round
+//     measured slower in the loop: 23.88 vs 23.54 us per iteration, profiles/r06e_fin_cell_ab.txt); p' = p S / (eps + sum_r p S)
 //     (:1021-1028) in place, or, SUMS, S_out = S.
 //   q part (joint model): as in fin_kernel.
 // ------------------------------------------------------------------------------------------
@@ -975,6 +1063,9 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
   const int wgx = blockIdx.x;
   Stamp st_{};
   st_.mark(0);
+#ifdef MMSBM_FIN_EMPTY  // measurement builds only (results invalid): the launch without its work
+  if (b >= 0) return;
+#endif
   if (wgx < n_gene_wg && ybuf) {
     constexpr int LPX = 64 / K, LY = K * LPX, YU = 16;  // lanes per component, lanes used
     const int lane = tid & 63, wv = tid >> 6;
@@ -988,11 +1079,50 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
     const int dg = deg[g];
     // the gene's Y range holds its observation entries and its X^0 partial rows (at fold0 ~100
     // entries of K words: one round of YU loads over LY lanes for most genes)
+    double S = 0.0;
+    if constexpr (K % 2 == 0) {
+      // even K (round 6): 16-byte loads (the wide coalesced form the memory pipe moves at full
+      // rate; the range and the sample's Y block start at even words).  Lane l < LW reads words
+      // 2 l, 2 l + 1 of each WW-word step, components 2 l mod K and 2 l + 1 mod K (WW = EPI K, a
+      // whole number of entries); YU2 steps in flight.
+      constexpr int EPI = 128 / K, WW = EPI * K, LW = WW / 2, YU2 = 8;
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      const long long wf = w0 + 2 * (lane < LW ? lane : 0);
+      double Sa = 0.0, Sb = 0.0;
+      if (lane < LW) {
+        for (long long wd = wf; wd < w1; wd += (long long)YU2 * WW) {
+          d2 v[YU2];
+#pragma unroll
+          for (int u = 0; u < YU2; ++u)
+            v[u] = *reinterpret_cast<const d2*>(yb + (wd + (long long)u * WW < w1 ? wd + (long long)u * WW : wf));
+#pragma unroll
+          for (int u = 0; u < YU2; ++u)
+            if (wd + (long long)u * WW < w1) {
+              Sa += v[u].x;
+              Sb += v[u].y;
+            }
+        }
+      }
+      double* __restrict__ yr2 = red + wv * 128;
+      yr2[2 * lane] = Sa;
+      yr2[2 * lane + 1] = Sb;
+      wave_lds_sync();
+      if (lane < K) {  // component x: words x + j K of a step, j in order
+        double Y = yr2[lane];
+#pragma unroll
+        for (int jj = 1; jj < EPI; ++jj) Y += yr2[lane + jj * K];
+        double X = Y;
+        if (nth_add) X += ad;
+        const size_t o = ((size_t)b * P + g) * K + lane;
+        if constexpr (SUMS) nth_out[o] = X;
+        else theta[o] = th * X / (double)dg;
+      }
+      return;
+    }
     const long long wf = w0 + (lane < LY ? lane : 0);
     double v0[YU];
 #pragma unroll
     for (int u = 0; u < YU; ++u) v0[u] = yb[wf + (long long)u * LY < w1 ? wf + (long long)u * LY : wf];
-    double S = 0.0;
     if (lane < LY) {
 #pragma unroll
       for (int u = 0; u < YU; ++u)

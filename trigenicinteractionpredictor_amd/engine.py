@@ -96,7 +96,7 @@ class EMEngine:
         _lib.check(self.lib.mmsbm_plan_info(self.ctx, which, v))
         keys = ("observations", "rows", "rows_stream0", "wg_stream0", "wg_stream12", "wg_spartial",
                 "partial_rows", "genes_per_wg_max", "v_genes", "partial_rows_stream0", "small_k",
-                "units", "plan_cus", "unit_target", "y_entries")
+                "units", "plan_cus", "unit_target", "y_entries", "gm_groups")
         return dict(zip(keys, [int(x) for x in v]))
 
     # ------------------------------------------------------------ parameters
@@ -162,8 +162,12 @@ class EMEngine:
                                         self._stream(stream)))
 
     def loglik_async(self, which: int = _lib.SET_TRAIN, out: torch.Tensor = None, stream=None):
+        """[B] device tensor; the kernels write the active prefix only, slots outside it read NaN
+        (the fill touches no word the launch writes, so its stream does not matter)."""
         if out is None:
             out = torch.empty(self.B, dtype=torch.float64, device=self.device)
+        if self.active < self.B:
+            out[self.active:] = float("nan")
         _lib.check(self.lib.mmsbm_loglik(self.ctx, which, _ptr(self.theta), _ptr(self.pr), _ptr(out),
                                          self._stream(stream)))
         return out
@@ -178,9 +182,12 @@ class EMEngine:
         return out
 
     def predict(self, ids: np.ndarray) -> np.ndarray:
-        """P(r=1) for each row of ids int32[n][3] -> [B][n] (host)."""
+        """P(r=1) for each row of ids int32[n][3] -> [B][n] (host); rows of slots outside the
+        active prefix are NaN (the kernel covers the active samples only)."""
         n = int(ids.shape[0])
         out = torch.empty((self.B, max(n, 1)), dtype=torch.float64, device=self.device)
+        if self.active < self.B:
+            out[self.active:] = float("nan")
         if n:
             ids_d = torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int32)).to(self.device)
             _lib.check(self.lib.mmsbm_predict(self.ctx, _ptr(ids_d), n, _ptr(self.theta), _ptr(self.pr),

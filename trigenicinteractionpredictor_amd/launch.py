@@ -5,10 +5,12 @@ The parent starts the ranks before it touches a GPU, with the environment torch.
 would give them (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR / MASTER_PORT on
 127.0.0.1), and waits on ALL of them at once: the first rank to fail has the survivors terminated
 (they would otherwise sit in a barrier or collective until its timeout) and its exit code is
-returned.  Pure Python, no torch import: safe before any GPU call.
+returned.  Pure Python, no torch import and no HIP call (visible_gpus reads sysfs): safe before
+any GPU call.
 """
 from __future__ import annotations
 
+import glob
 import os
 import socket
 import subprocess
@@ -54,8 +56,23 @@ def spawn_ranks(cmd, n: int) -> int:
     return wait_ranks(procs)
 
 
-def visible_gpus() -> int:
-    """GPUs this process may use, counted without initialising HIP (torch.cuda.device_count()
-    does not create a context on this image)."""
-    import torch
-    return torch.cuda.device_count()
+def visible_gpus():
+    """GPUs this process may use, counted without touching HIP (the launcher runs this before it
+    spawns the ranks, and must not initialise the GPU in the parent): the KFD topology nodes with
+    a GPU id, capped by the *_VISIBLE_DEVICES lists the HIP runtime honours.  None when the
+    topology is not readable (the ranks then check with the runtime's own count)."""
+    files = glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id")
+    if not files:
+        return None
+    n = 0
+    for f in files:
+        try:
+            with open(f) as fh:
+                n += int(fh.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            pass
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n

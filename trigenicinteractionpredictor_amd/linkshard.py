@@ -67,6 +67,7 @@ class LinkShardedEM:
         self.nth = self.buf[:n_th].view(B, P, K)
         self.S = self.buf[n_th:].view(B, R, K ** 3)
         self.B = B
+        self.active = B
         self.device = engine.device
 
     def _sum(self, t):
@@ -103,12 +104,20 @@ class LinkShardedEM:
         self.engine.move_slot(dst, src)
 
     def set_active(self, n):
+        """Shrink (or restore) the active prefix: accumulate / mstep cover samples [0, n) only, so
+        the collective does too (the inactive slots' sums are stale and are never reduced)."""
         self.engine.set_active(n)
+        self.active = int(n)
 
     def iterate(self, n_iters: int = 1):
+        a = self.active
         for _ in range(int(n_iters)):
             self.engine.accumulate(self.nth, self.S)
-            self._sum(self.buf)
+            if a == self.B:
+                self._sum(self.buf)          # one collective over the whole buffer
+            else:                            # the active prefix of each part (B is the leading dim)
+                self._sum(self.nth[:a])
+                self._sum(self.S[:a])
             self.engine.mstep(self.nth, self.S)
 
     def loglik(self, which: int = TRAIN) -> np.ndarray:
