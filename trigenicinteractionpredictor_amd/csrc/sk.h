@@ -44,10 +44,6 @@ enum { SK_A = 0, SK_LL = 1, SK_B = 2, SK_U = 3 };
 #ifndef MMSBM_SK_PVS
 #define MMSBM_SK_PVS 1  // P^s rows at an odd stride (0: K^2, round 3), see SKT::PVS
 #endif
-#ifndef MMSBM_SK_Z16
-#define MMSBM_SK_Z16 0  // 1: SK_U's Z of four chunks per v_mfma_f64_16x16x4f64, no LDS in the chunk loop
-                        // (round 6, measured slower: fused 19.9 vs 17.3 us, profiles/r06b_z16_ab.txt)
-#endif
 #ifndef MMSBM_SK_GHOIST
 #define MMSBM_SK_GHOIST 0  // 1: the first block's theta gathers before the V tables (after the barrier)
 #endif
@@ -121,7 +117,6 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     double eps, const int4* __restrict__ urec1, const int* __restrict__ udesc1, int L1) {
   using T = SKT<K>;
   constexpr int NG = T::NG, K2 = T::K2, K3 = T::K3, NCT = T::NCT, NCG = T::NCG, SLOT = T::SLOT;
-  constexpr bool Z16 = MODE == SK_U && MMSBM_SK_Z16;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -249,13 +244,6 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     st_.t[5] = (unsigned long long)(c1 - c0);
     st_.t[4] = (unsigned long long)nst;
     const auto& ds = un.ds;
-    auto stretch_end = [&](int t) {  // first chunk after stretch t (scalar selects, constant indices)
-      int e = c1;
-#pragma unroll
-      for (int i = 1; i < GUK; ++i)
-        if (t + 1 == i && i < nst) e = ds[i];
-      return e;
-    };
     const int2* __restrict__ rec = REC;
     const int colc = col < K ? col : K - 1;
     const unsigned cb = (unsigned)colc * 8u;
@@ -316,26 +304,44 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
       for (int i = 0; i < (T::THL + 63) / 64; ++i)
         if (lane + 64 * i < T::THL) THl[lane + 64 * i] = 0.0;
     }
+    if constexpr (MODE != SK_B) TRl[64 + lane] = 0.0;  // (load_v's zero words)
     wave_lds_sync();
     st_.mark(1);
 
     const double* __restrict__ vrow = MSl + col * K + hi;
     const double* __restrict__ cw = MODE == SK_B ? AUX : DL;
     d4v m16 = d4v{0.0, 0.0, 0.0, 0.0};  // the running stretch's M (persists across blocks)
-    int t = 0;
-    int send = stretch_end(0);
+    int t = 0;                          // the running stretch (phase 2)
     double vb[NG];  // B of Z: V_vt[b = col][h = 4 hs + hi] of the running stretch (phase 1)
-    auto load_v = [&](int tv_) {  // (zero for b = col >= K and h >= K: no mask on the products)
+    // The V operand's LDS word per (lane, h tile): the running stretch's slot where b = col < K and
+    // h = 4 hs + hi < K, else a zeroed word (the second transpose buffer, TRl + 64, zeroed before
+    // the V tables and never written after), so the loads need neither a mask nor a select: plain
+    // ds_reads issued at a stretch change and first waited on by the next chunk's MFMA (round 6:
+    // the masked form made each stretch change wait an LDS round trip inside the chunk chain)
+    int voff[NG], vstr[NG];
 #pragma unroll
-      for (int hs = 0; hs < NG; ++hs) {
-        const double x = vrow[tv_ * SLOT + 4 * hs];
-        vb[hs] = kcol && 4 * hs + hi < K ? x : 0.0;
-      }
+    for (int hs = 0; hs < NG; ++hs) {
+      const bool ok = kcol && 4 * hs + hi < K;
+      voff[hs] = ok ? (int)(MSl - smem) + col * K + hi + 4 * hs : (int)(TRl + 64 - smem);
+      vstr[hs] = ok ? SLOT : 0;
+    }
+    auto load_v = [&](int tv_) {
+#pragma unroll
+      for (int hs = 0; hs < NG; ++hs) vb[hs] = smem[voff[hs] + tv_ * vstr[hs]];
     };
-    int vt = 0, vsend = send;
+    int vt = 0;  // the running stretch (phase 1: its V operand)
     if constexpr (MODE != SK_B) load_v(0);
     for (int b0 = 0; b0 < c1; b0 += LC) {  // (uniform; one block for units of <= LC chunks)
       const int nb = c1 - b0;               // chunks left (this block: min(nb, LC))
+      // bit q: chunk b0 + q ends a stretch other than the unit's last (one scalar test per chunk
+      // instead of tracking the next stretch's end through a select chain over ds[]; round 6)
+      unsigned endm = 0;
+#pragma unroll
+      for (int i = 1; i < GUK; ++i) {
+        const int e = ds[i] - 1 - b0;
+        if (i < nst && e >= 0 && e < LC) endm |= 1u << e;
+      }
+      endm = __builtin_amdgcn_readfirstlane(endm);
       if (b0 > 0) {  // this block's records (loaded during the last one) into the wave's LDS
         wave_lds_sync();
         stage_block(bk);
@@ -343,87 +349,6 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
       }
       if (nb > LC) load_block(b0 / LC + 1, bk);  // the next block's records, in flight meanwhile
       if (!MMSBM_SK_GHOIST || b0 > 0) gather(nb);
-      if constexpr (Z16) {
-        // ---- Z of four chunks at once on v_mfma_f64_16x16x4f64, no LDS in the chunk loop (round 6).
-        // m = the 16 observations of chunks 4 g .. 4 g + 3 (record 16 g + m), k = h, n = b:
-        //   A[m][k] = theta_v(record 16 g + m)[4 hs + k]: gathered straight into lane (k = hi, m = col)
-        //   B[k][n] = V_vt[b = n][h = 4 hs + k] = vb[hs] (lane (hi, col), as the 4x4x4 path)
-        //   D[m = hi + 4 i][n = col] in element i = Z of (chunk 4 g + i, obs hi)[b = col]
-        // so lane (hi, col) holds the Z row of observation hi of each chunk in the layout of ga: d is
-        // the DPP row sum of ga * Z, c = n / d in the 16 lanes of the observation (the layout the M
-        // MFMA takes its c from), and no transpose, fence or d / c word goes through LDS.  A group
-        // crossing a stretch end takes the Z of each stretch for the chunks of that stretch.
-        // (A rows past the unit's end read a valid record: load_block clamps; they are not used.)
-        constexpr int NGR = LC / 4;
-        double za[NGR][NG];
-        auto load_za = [&](int g) {
-          if (4 * g < nb) {  // (uniform)
-            const int vg = rec[16 * g + col].y;
-            const char* __restrict__ thb = reinterpret_cast<const char*>(th);
-#pragma unroll
-            for (int hs = 0; hs < NG; ++hs) {  // (h >= K: a finite word against the zero B rows)
-              const unsigned hc = (unsigned)(4 * hs + hi < K ? 4 * hs + hi : K - 1) * 8u;
-              za[g][hs] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)vg, K * 8u) + hc));
-            }
-          } else {
-#pragma unroll
-            for (int hs = 0; hs < NG; ++hs) za[g][hs] = 0.0;
-          }
-        };
-        load_za(0);  // (then one group ahead: two groups' operands live, not four)
-        auto zmm = [&](int g) {
-          d4v D = d4v{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int hs = 0; hs < NG; ++hs) D = mfma16(za[g][hs], vb[hs], D);
-          return D;
-        };
-#pragma unroll
-        for (int g = 0; g < NGR; ++g) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (g + 1 < NGR) load_za(g + 1);
-          if (4 * g < nb) {  // (uniform)
-            const int clo = b0 + 4 * g, chi = b0 + 4 * g + (nb - 4 * g < 4 ? nb - 4 * g : 4);
-            d4v Z = zmm(g);
-            while (vsend < chi) {  // (uniform) a stretch ends inside the group: the next one's V
-              const int vstart = vsend;
-              ++vt;
-              vsend = stretch_end(vt);
-              load_v(vt);
-              const d4v Zn = zmm(g);
-#pragma unroll
-              for (int i = 0; i < 4; ++i)
-                if (clo + i >= vstart) Z[i] = Zn[i];
-            }
-            if (vsend == chi && vt + 1 < nst) {  // the next group starts the next stretch
-              ++vt;
-              vsend = stretch_end(vt);
-              load_v(vt);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int q = 4 * g + i;
-              if (q < nb) {
-                const int n0 = __builtin_amdgcn_readlane(wlane, 4 * q), n1 = __builtin_amdgcn_readlane(wlane, 4 * q + 1);
-                const int n2 = __builtin_amdgcn_readlane(wlane, 4 * q + 2), n3 = __builtin_amdgcn_readlane(wlane, 4 * q + 3);
-                const int nq = hi == 0 ? n0 : hi == 1 ? n1 : hi == 2 ? n2 : n3;
-                const double d = row16_sum(ga[q] * Z[i]) + eps;
-                const double c = sk_div((double)nq, d);
-                m16 = mfma16(ga[q], c * gv[q], m16);
-                if (b0 + q + 1 == send) {  // stretch t done: its M row into slot t
-#pragma unroll
-                  for (int j = 0; j < 4; ++j) {
-                    const int x = hi + 4 * j;
-                    if (x < K && kcol) MSl[t * SLOT + x * K + col] = m16[j];
-                  }
-                  m16 = d4v{0.0, 0.0, 0.0, 0.0};
-                  ++t;
-                  send = stretch_end(t);
-                }
-              }
-            }
-          }
-        }
-      } else {
       if constexpr (MODE != SK_B) {
         // ---- d of every observation of the block.  Per chunk: Z[obs hi][b = col] =
         // sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA (A = theta_v(obs lo)[4 hs + hi], the transpose
@@ -450,10 +375,9 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
 #pragma unroll
               for (int hs = 0; hs < NG; ++hs) z = mfma4(TRl[16 * lo + 4 * hs + hi], vb[hs], z);
               R = mfma16(ga[q] * z, col == 4 * u + hi ? 1.0 : 0.0, R);
-              if (q < nb && b0 + q + 1 == vsend) {  // the next stretch's V operand
+              if (q < nb && ((endm >> q) & 1u)) {  // the next stretch's V operand
                 ++vt;
-                vsend = stretch_end(vt);
-                if (vt < nst) load_v(vt);
+                load_v(vt);
               }
             }
             double sr = (R[0] + R[1]) + (R[2] + R[3]);
@@ -487,10 +411,9 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
             // (the 16 lanes of a row hold the same bits and store the same word; storing from one
             // lane per row measured no faster, r03u)
             DL[q * 4 + hi] = row16_sum(ga[q] * z) + eps;
-            if (b0 + q + 1 == vsend) {  // the next stretch's V operand
+            if ((endm >> q) & 1u) {  // the next stretch's V operand
               ++vt;
-              vsend = stretch_end(vt);
-              if (vt < nst) load_v(vt);
+              load_v(vt);
             }
           }
         }
@@ -523,7 +446,7 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
         for (int q = 0; q < LC; ++q) {
           if (q < nb) {
             m16 = mfma16(ga[q], cw[q * 4 + hi] * gv[q], m16);
-            if (b0 + q + 1 == send) {  // stretch t done: its M row into slot t
+            if (((endm >> q) & 1u) || b0 + q + 1 == c1) {  // stretch t done: its M row into slot t
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 const int x = hi + 4 * i;
@@ -531,12 +454,10 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
               }
               m16 = d4v{0.0, 0.0, 0.0, 0.0};
               ++t;
-              send = stretch_end(t);
             }
           }
         }
       }
-      }  // (Z16)
     }
     st_.mark(2);
   }
@@ -705,7 +626,7 @@ struct SKY {
   using T = SKT<K>;
   // per wave: slots, the block's (u, v) genes, pivot rows, the block's Y entries, one transpose
   // buffer
-  static constexpr int WAVE = T::GUK * T::SLOT + SK_ROWS + T::THL + SK_ROWS + 64;
+  static constexpr int WAVE = T::GUK * T::SLOT + SK_ROWS + T::THL + SK_ROWS + 64 + 16;  // (+ zero words)
   static constexpr int LDS = (T::PSD + NW * WAVE) * 8;
   static_assert(LDS <= 80 * 1024, "two SK_Y workgroups per CU");
   // the unguarded Z' operand reads (rows b < 4 NG of the last slot, columns up to 15) stay inside
@@ -743,6 +664,7 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
   double* THl = wl + GUK * SLOT + SK_ROWS;                 // pivot theta rows [GUK][4 NG]
   int2* YE = reinterpret_cast<int2*>(THl + T::THL);        // the block's Y entries (slot 1, slot 2)
   double* TRl = THl + T::THL + SK_ROWS;                    // the Z / Z' operand transpose
+  double* ZRl = TRl + 64;                                  // 16 zero words (load_v's masked lanes)
   double* __restrict__ yb = ybuf + (size_t)b * (n_y + 1) * K;
   (void)xpart;
   (void)n_prows;
@@ -838,13 +760,6 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
     st_.t[5] = (unsigned long long)c1;
     st_.t[4] = (unsigned long long)nst;
     const auto& ds = un.ds;
-    auto stretch_end = [&](int t) {
-      int e = c1;
-#pragma unroll
-      for (int i = 1; i < GUK; ++i)
-        if (t + 1 == i && i < nst) e = ds[i];
-      return e;
-    };
     const auto& tv = un.tv;
     // ---- V_g[cell] = sum_a theta_g[a] P^0[a][cell] for the unit's genes into their slots (every
     // word of the GUK slots written: zero past K^2 and for absent stretches); pivot theta rows to
@@ -868,6 +783,7 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
         if (blk == 0) THl[(4 * tt + lo) * 4 * NG + 4 * as + hi] = tv[tt][as];
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (lane < 16) ZRl[lane] = 0.0;
     wave_lds_sync();
     st_.mark(1);
 
@@ -877,20 +793,33 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
     const double* __restrict__ vcol = MSl + hi * K + col;
     d4v m16 = d4v{0.0, 0.0, 0.0, 0.0};
     int t = 0;
-    int send = stretch_end(0);
     double vb[NG], vbt[NG];
+    // (the Z operand from the slot or a zero word, as in sk_pass_kernel; Z' needs no mask)
+    int voff[NG], vstr[NG];
+#pragma unroll
+    for (int hs = 0; hs < NG; ++hs) {
+      const bool ok = kcol && 4 * hs + hi < K;
+      voff[hs] = ok ? (int)(MSl - smem) + col * K + hi + 4 * hs : (int)(ZRl - smem);
+      vstr[hs] = ok ? SLOT : 0;
+    }
     auto load_v = [&](int tv_) {
 #pragma unroll
       for (int hs = 0; hs < NG; ++hs) {
-        const double x = vrow[tv_ * SLOT + 4 * hs];
-        vb[hs] = kcol && 4 * hs + hi < K ? x : 0.0;
+        vb[hs] = smem[voff[hs] + tv_ * vstr[hs]];
         vbt[hs] = vcol[tv_ * SLOT + 4 * hs * K];
       }
     };
-    int vt = 0, vsend = send;
+    int vt = 0;
     load_v(0);
     for (int b0 = 0; b0 < c1; b0 += LC) {
       const int nb = c1 - b0;
+      unsigned endm = 0;  // bit q: chunk b0 + q ends a stretch other than the unit's last
+#pragma unroll
+      for (int i = 1; i < GUK; ++i) {
+        const int e = ds[i] - 1 - b0;
+        if (i < nst && e >= 0 && e < LC) endm |= 1u << e;
+      }
+      endm = __builtin_amdgcn_readfirstlane(endm);
       // ---- theta gathers: every value of the block at once, straight into the registers of the
       // MFMA operands (lane (obs hi, col): theta_j and theta_k of its observation, column col;
       // col >= K a finite copy of column K - 1, masked where a product needs it); the first
@@ -934,12 +863,12 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
             yb[(size_t)ey.y * K + col] = c * zp;
           }
           m16 = mfma16(ga[q], c * gv[q], m16);
-          if (b0 + q + 1 == vsend) {  // the next stretch's V operands
+          const bool ends = (endm >> q) & 1u;
+          if (ends) {  // the next stretch's V operands
             ++vt;
-            vsend = stretch_end(vt);
-            if (vt < nst) load_v(vt);
+            load_v(vt);
           }
-          if (b0 + q + 1 == send) {
+          if (ends || b0 + q + 1 == c1) {  // stretch t done: its M row into slot t
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int x = hi + 4 * i;
@@ -947,7 +876,6 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
             }
             m16 = d4v{0.0, 0.0, 0.0, 0.0};
             ++t;
-            send = stretch_end(t);
           }
         }
       }
@@ -1024,7 +952,8 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
 //     order; lane x < K adds that to its X^0 partial rows (stream 0) and updates theta.
 //   cell part: 16 cells x 16 parts per workgroup: S_r[cell] = sum of the rating's S partials
 //     (one per stream-0 workgroup), parts combined in order (every rating's loads in one round
-//     measured slower in the loop: 23.88 vs 23.54 us per iteration, profiles/r06e_fin_cell_ab.txt); p' = p S / (eps + sum_r p S)
+//     measured slower in the loop: 23.88 vs 23.54 us per iteration,
+//     profiles/r06e_fin_cell_gm_ab.txt); p' = p S / (eps + sum_r p S)
 //     (:1021-1028) in place, or, SUMS, S_out = S.
 //   q part (joint model): as in fin_kernel.
 // ------------------------------------------------------------------------------------------
