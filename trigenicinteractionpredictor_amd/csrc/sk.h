@@ -255,18 +255,22 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
     // so no select waits for a load here
     double ga[LC], gv[LC];
     auto gather = [&](int nb) {
+      // Every chunk of the block loads, a short block too (chunks past the unit's end read the
+      // clamped records load_block staged: valid genes, values never used): with no branch between
+      // them the 16 record reads go out together and each chunk waits for its own two loads only
+      // (round 6: per-chunk guards made the compiler wait for every load of the block before the
+      // first chunk, and read the records one LDS round trip at a time)
+      (void)nb;
+      int2 rh[LC];
+#pragma unroll
+      for (int i = 0; i < LC; ++i) rh[i] = rec[i * 4 + hi];  // (u gene, v gene): make_slots orders them
 #pragma unroll
       for (int i = 0; i < LC; ++i) {
-        ga[i] = 0.0;  // (chunks past the unit's end stay zero)
-        gv[i] = 0.0;
-        if (i < nb) {  // uniform guard: a short block issues only its own loads
-          const int2 rh = rec[i * 4 + hi];  // (u gene, v gene): make_slots orders them
-          // (32-bit byte offsets from the sample's theta base: one 24-bit multiply-add per address;
-          // col >= K reads a finite copy of column K - 1)
-          const char* __restrict__ thb = reinterpret_cast<const char*>(th);
-          ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
-          gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
-        }
+        // (32-bit byte offsets from the sample's theta base: one 24-bit multiply-add per address;
+        // col >= K reads a finite copy of column K - 1)
+        const char* __restrict__ thb = reinterpret_cast<const char*>(th);
+        ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh[i].x, K * 8u) + cb));
+        gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh[i].y, K * 8u) + cb));
       }
     };
     if constexpr (MMSBM_SK_GHOIST) gather(c1 < LC ? c1 : LC);  // (in flight during the V tables)
@@ -347,8 +351,8 @@ __global__ __launch_bounds__(NT, 4) void sk_pass_kernel(
         stage_block(bk);
         wave_lds_sync();
       }
-      if (nb > LC) load_block(b0 / LC + 1, bk);  // the next block's records, in flight meanwhile
       if (!MMSBM_SK_GHOIST || b0 > 0) gather(nb);
+      if (nb > LC) load_block(b0 / LC + 1, bk);  // the next block's records, in flight meanwhile
       if constexpr (MODE != SK_B) {
         // ---- d of every observation of the block.  Per chunk: Z[obs hi][b = col] =
         // sum_h theta_v(obs hi)[h] V_t[b][h] on MFMA (A = theta_v(obs lo)[4 hs + hi], the transpose
@@ -734,17 +738,20 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
   const unsigned cb = (unsigned)colc * 8u;
   const bool kcol = col < K;
   double ga[LC], gv[LC];
-  auto gather = [&](int nb) {
+  auto gather = [&](int nb) {  // (every chunk of the block, as in sk_pass_kernel; nb = 0: none)
+    if (nb > 0) {  // (uniform)
+      int2 rh[LC];
 #pragma unroll
-    for (int i = 0; i < LC; ++i) {
-      ga[i] = 0.0;
-      gv[i] = 0.0;
-      if (i < nb) {  // (uniform)
-        const int2 rh = REC[i * 4 + hi];
+      for (int i = 0; i < LC; ++i) rh[i] = REC[i * 4 + hi];
+#pragma unroll
+      for (int i = 0; i < LC; ++i) {
         const char* __restrict__ thb = reinterpret_cast<const char*>(th);
-        ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.x, K * 8u) + cb));
-        gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh.y, K * 8u) + cb));
+        ga[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh[i].x, K * 8u) + cb));
+        gv[i] = *reinterpret_cast<const double*>(thb + (__umul24((unsigned)rh[i].y, K * 8u) + cb));
       }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LC; ++i) ga[i] = gv[i] = 0.0;
     }
   };
   gather(un.nst > 0 ? (un.c1 < LC ? un.c1 : LC) : 0);
