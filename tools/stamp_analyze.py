@@ -35,6 +35,31 @@ def main(path, bench_json=None):
         print("  life   %s" % q(life))
         print("  phase1 %s" % q(ph1))
         print("  phase2 %s" % q(ph2))
+        if name == "fin" and (t[:, 9] != 0).all():
+            # small-K fin (sk_fin_kernel): chip-wide start / end against the E-step launch's waves
+            # (the same 100 MHz clock): the gap between the two launches and fin's own span
+            ea = h[0]
+            ea = ea[ea[:, 0] != 0]
+            rt0 = ea[:, 8].min() if len(ea) else t[:, 8].min()
+            e_end = ea[:, 9].max() if len(ea) else rt0
+            print("  start (ns from the E-step's first wave) %s" % q((t[:, 8] - rt0) * 10))
+            print("  end   (ns from the E-step's first wave) %s" % q((t[:, 9] - rt0) * 10))
+            print("  E-step's last wave ends at %d ns; fin's first wave starts %d ns later, its last "
+                  "ends %d ns after that" % ((e_end - rt0) * 10, (t[:, 8].min() - e_end) * 10,
+                                             (t[:, 9].max() - e_end) * 10))
+            wg = idx // 4
+            ngw = int(sys.argv[3]) if len(sys.argv) > 3 else 59  # gene workgroups (P K / 256)
+            for pname, sel in (("gene", wg < ngw), ("cell", wg >= ngw)):
+                if sel.any():
+                    tt = t[sel]
+                    print("  [%s] %d waves: start ns %s | end ns %s | life ns %s" % (
+                        pname, sel.sum(), q((tt[:, 8] - rt0) * 10), q((tt[:, 9] - rt0) * 10),
+                        q((tt[:, 9] - tt[:, 8]) * 10)))
+                    for k in (1, 2, 3):  # cycles from the start to marks 1-3 (0: not marked)
+                        if (tt[:, k] != 0).any():
+                            print("      ->mark%d cycles %s" % (k, q(np.where(tt[:, k] != 0, tt[:, k] - tt[:, 0], 0))))
+                    print("      ->end   cycles %s" % q(tt[:, 7] - tt[:, 0]))
+            continue
         if name == "fin":
             print("  ->sync %s" % q(t[:, 4] - t[:, 0]))
             print("  ->rows %s" % q(t[:, 5] - t[:, 0]))

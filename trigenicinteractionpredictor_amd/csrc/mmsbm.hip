@@ -140,6 +140,23 @@ constexpr int lds_target(int K) {
 #define MMSBM_YALIGN 4
 #endif
 constexpr int y_stride(int K) { return (K + MMSBM_YALIGN - 1) / MMSBM_YALIGN * MMSBM_YALIGN; }
+// Y entry stores (pass A) and loads (upd) plain or non-temporal: bit 1 stores, bit 2 loads.
+// Non-temporal loads in upd: K=30 on 10M links upd 895 -> 807 us (the 5.1 GB stream no longer
+// displaces the L2's theta / X-row lines); non-temporal stores in pass A within noise, and
+// non-temporal loads of the small-K SK_Y entries (92 MB, just written, on die) slower (fin 19.5 ->
+// 21.8 us at K=10 x 8): profiles/r06p_fin_ynt_ab.txt, r06q_fin_butterfly_ab.txt
+#ifndef MMSBM_YNT
+#define MMSBM_YNT 2
+#endif
+__device__ __forceinline__ void y_st(double* p, double v) {
+  if constexpr (MMSBM_YNT & 1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+typedef double yd2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ yd2 y_ld2(const yd2* p) {
+  if constexpr (MMSBM_YNT & 2) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 
 // Pass-kernel occupancy hint: 1 leaves the compiler free (K = 25-32 take 132-134 VGPRs, so one
 // 8-wave workgroup per CU although the LDS would fit two); 4 caps it at 128 VGPRs (4 waves per
@@ -605,7 +622,7 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
 #pragma unroll
           for (int bg = 0; bg < T::NBG; ++bg) {
             const int bb = 16 * bg + 4 * blk + lo;
-            if (bb < YS && !(MMSBM_ABL & 1)) yb[(size_t)e1 * YS + bb] = c * zb[bg];
+            if (bb < YS && !(MMSBM_ABL & 1)) y_st(yb + (size_t)e1 * YS + bb, c * zb[bg]);
           }
 #pragma unroll
           for (int hg = 0; hg < T::NBG; ++hg) {
@@ -620,7 +637,7 @@ __global__ __launch_bounds__(KT<K>::NTK) __attribute__((amdgpu_waves_per_eu(KT<K
             }
             if (ZSPLIT) z2 += z2o;
             const int hh = 16 * hg + 4 * blk + lo;
-            if (hh < YS && !(MMSBM_ABL & 1)) yb[(size_t)e2 * YS + hh] = c * z2;
+            if (hh < YS && !(MMSBM_ABL & 1)) y_st(yb + (size_t)e2 * YS + hh, c * z2);
             else if (MMSBM_ABL & 1) ll += z2;  // (keep Z' live)
           }
           // ---- M += c th_u (x) th_v over the chunk's 4 observations: one v_mfma_f64_16x16x4 per
@@ -1060,7 +1077,7 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
         d2 v[YU2];
 #pragma unroll
         for (int u = 0; u < YU2; ++u)
-          v[u] = *reinterpret_cast<const d2*>(yb + (wd + (long long)u * WW < w1 ? wd + (long long)u * WW : wf));
+          v[u] = y_ld2(reinterpret_cast<const d2*>(yb + (wd + (long long)u * WW < w1 ? wd + (long long)u * WW : wf)));
 #pragma unroll
         for (int u = 0; u < YU2; ++u)
           if (wd + (long long)u * WW < w1) {
@@ -1891,7 +1908,9 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   }
   if (const char* u = getenv("MMSBM_UNITS")) {
     int a = 0, b = 0;
-    if (sscanf(u, "%d,%d", &a, &b) == 2 && a > 0 && b > 0) {
+    const int n = sscanf(u, "%d,%d", &a, &b);
+    if (n == 1) b = a;  // (one number: both targets)
+    if (n >= 1 && a > 0 && b > 0) {
       units_a = a;
       units_b = b;
     }

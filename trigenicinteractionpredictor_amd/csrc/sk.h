@@ -957,14 +957,18 @@ __global__ __launch_bounds__(NT, 4) void sky_pass_kernel(
 //     block of K-word rows, Plan::yptr) are summed by lanes l < K floor(64 / K), lane l taking
 //     words l, l + LY, ... (component l mod K), the lanes of one component then added in lane
 //     order; lane x < K adds that to its X^0 partial rows (stream 0) and updates theta.
-//   cell part: 16 cells x 16 parts per workgroup: S_r[cell] = sum of the rating's S partials
-//     (one per stream-0 workgroup), parts combined in order (every rating's loads in one round
-//     measured slower in the loop: 23.88 vs 23.54 us per iteration,
-//     profiles/r06e_fin_cell_gm_ab.txt); p' = p S / (eps + sum_r p S)
+//   cell part: SKF_CW cells x SKF_NPART parts per workgroup: S_r[cell] = sum of the rating's S
+//     partials (one per stream-0 workgroup), parts combined in order, two ratings' loads in one
+//     round; p' = p S / (eps + sum_r p S)
 //     (:1021-1028) in place, or, SUMS, S_out = S.
 //   q part (joint model): as in fin_kernel.
 // ------------------------------------------------------------------------------------------
-constexpr int SKF_NT = 256, SKF_CW = 16, SKF_NPART = 16;
+// cell part: SKF_CW cells x SKF_NPART parts per workgroup, SKF_SB partial loads per batch (round 6:
+// 8 x 32 x 4 instead of 16 x 16 x 16: a part's few partials (fold0: 2-3 of 88 per rating) without
+// the clamped duplicate loads that kept the address units of each cell workgroup's CU busy; the
+// 32 parts are added by a butterfly in each wave, then the 4 waves in order)
+constexpr int SKF_NT = 256, SKF_CW = 8, SKF_NPART = 32, SKF_SB = 4;
+static_assert(SKF_CW * SKF_NPART == SKF_NT, "fin cell part: one (cell, part) per thread");
 
 // sum of gene g's X partials (component x): its gene-major range [gptr[g], gptr[g + 1]) of
 // partial rows ((stream, rating, row) order, Plan::prow_g), 8 loads in flight (a hub gene's pivot
@@ -1001,6 +1005,9 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
   st_.mark(0);
 #ifdef MMSBM_FIN_EMPTY  // measurement builds only (results invalid): the launch without its work
   if (b >= 0) return;
+#endif
+#ifdef MMSBM_FIN_ONLY  // measurement builds only (results invalid): 1 = gene workgroups only, 2 = cell only
+  if ((MMSBM_FIN_ONLY == 1) != (wgx < n_gene_wg)) return;
 #endif
   if (wgx < n_gene_wg && ybuf) {
     constexpr int LPX = 64 / K, LY = K * LPX, YU = 16;  // lanes per component, lanes used
@@ -1096,45 +1103,75 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
     const double ad = nth_add ? nth_add[((size_t)b * P + g) * K + x] : 0.0;
     const int dg = deg[g];
     double X = sk_gene_sum(xb, gptr, g, x, K);
+    st_.mark(1);
     if (nth_add) X += ad;
     const size_t o = ((size_t)b * P + g) * K + x;
     if constexpr (SUMS) nth_out[o] = X;
     else theta[o] = th * X / (double)dg;
+    st_.mark(7);
+    st_.flush(2, ((long long)b * gridDim.x + wgx) * (SKF_NT / 64) + (tid >> 6), tid & 63);
     return;
   }
   if (wgx < n_gene_wg + NCW) {
     const int cl = tid % SKF_CW, part = tid / SKF_CW;
     const int cell = (wgx - n_gene_wg) * SKF_CW + cl;
     const int cc = cell < K3 ? cell : 0;
+    // the S partial loads of two ratings go out together (round 6: one dependent round for R = 2
+    // instead of one per rating, with the same sums: each rating's parts and their order are
+    // unchanged); p (for p') is loaded after them, off their path
+    auto part_sum = [&](int r, double (&v)[SKF_SB], int& s0, int& s1) {  // loads of rating r's part
+      const int n = spr.hi[r] - spr.lo[r];
+      s0 = spr.lo[r] + n * part / SKF_NPART;
+      s1 = spr.lo[r] + n * (part + 1) / SKF_NPART;
+#pragma unroll
+      for (int u = 0; u < SKF_SB; ++u)
+        v[u] = spart[((size_t)b * n_wg_a + (s0 + u < s1 ? s0 + u : s0)) * K3 + cc];
+    };
+    // a part's sum, then the wave's 8 parts (lane bits 3-5) by a butterfly (commutative pairs: every
+    // lane gets the same bits), parked per (wave, rating, cell) for the in-order sum over waves
+    auto finish = [&](int r, const double (&v)[SKF_SB], int s0, int s1) {
+      double S = 0.0;
+#pragma unroll
+      for (int u = 0; u < SKF_SB; ++u) S += s0 + u < s1 ? v[u] : 0.0;
+      for (int sp = s0 + SKF_SB; sp < s1; sp += SKF_SB) {  // (parts longer than one batch)
+        double w[SKF_SB];
+#pragma unroll
+        for (int u = 0; u < SKF_SB; ++u) {
+          const double xv = spart[((size_t)b * n_wg_a + (sp + u < s1 ? sp + u : s0)) * K3 + cc];
+          w[u] = sp + u < s1 ? xv : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < SKF_SB; ++u) S += w[u];
+      }
+      S += __shfl_xor(S, 8, 64);
+      S += __shfl_xor(S, 16, 64);
+      S += __shfl_xor(S, 32, 64);
+      if ((tid & 63) < SKF_CW) red[((tid >> 6) * MAX_R + r) * SKF_CW + cl] = S;
+    };
+    for (int r = 0; r < R; r += 2) {
+      double va[SKF_SB], vb[SKF_SB];
+      int a0, a1, b0 = 0, b1 = 0;
+      part_sum(r, va, a0, a1);
+      const bool two = r + 1 < R;  // (uniform)
+      if (two) part_sum(r + 1, vb, b0, b1);
+      finish(r, va, a0, a1);
+      if (two) finish(r + 1, vb, b0, b1);
+      st_.mark(1 + (r < 1 ? 0 : 1));
+    }
     double po[MAX_R];
 #pragma unroll
     for (int r = 0; r < MAX_R; ++r) po[r] = pr[((size_t)b * R + (r < R ? r : R - 1)) * K3 + cc];
-    for (int r = 0; r < R; ++r) {
-      const int n = spr.hi[r] - spr.lo[r];
-      const int s0 = spr.lo[r] + n * part / SKF_NPART, s1 = spr.lo[r] + n * (part + 1) / SKF_NPART;
-      double S = 0.0;
-      for (int sp = s0; sp < s1; sp += 16) {
-        double v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const double xv = spart[((size_t)b * n_wg_a + (sp + u < s1 ? sp + u : s0)) * K3 + cc];
-          v[u] = sp + u < s1 ? xv : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) S += v[u];
-      }
-      red[(r * SKF_NPART + part) * SKF_CW + cl] = S;
-    }
     __syncthreads();
+    st_.mark(3);
     if (part == 0 && cell < K3) {
       double npr[MAX_R];
       double den = eps;
 #pragma unroll
       for (int r = 0; r < MAX_R; ++r) {
         if (r < R) {
-          double S = red[(r * SKF_NPART) * SKF_CW + cl];
+          double S = red[r * SKF_CW + cl];
 #pragma unroll
-          for (int q = 1; q < SKF_NPART; ++q) S += red[(r * SKF_NPART + q) * SKF_CW + cl];
+          for (int q = 1; q < SKF_NT / 64; ++q) S += red[(q * MAX_R + r) * SKF_CW + cl];
           if constexpr (SUMS) {
             S_out[((size_t)b * R + r) * K3 + cell] = S;
           } else {
@@ -1149,6 +1186,8 @@ __global__ __launch_bounds__(SKF_NT) void sk_fin_kernel(
           if (r < R) pr[((size_t)b * R + r) * K3 + cell] = npr[r] / den;
       }
     }
+    st_.mark(7);
+    st_.flush(2, ((long long)b * gridDim.x + wgx) * (SKF_NT / 64) + (tid >> 6), tid & 63);
     return;
   }
   // joint model q cells (include/mmsbm_pairs.h): 64 cells of qr per workgroup, 4 threads per cell
