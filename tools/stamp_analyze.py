@@ -87,6 +87,8 @@ def main(path, bench_json=None):
                     print("    end ns    %s" % q((tt[:, 9] - rt0) * 10))
                     print("    life ns   %s" % q((tt[:, 9] - tt[:, 8]) * 10))
                     print("    prologue  %s" % q(tt[:, 1] - tt[:, 0]))
+                    print("      ->p     %s" % q(tt[:, 6] - tt[:, 0]))
+                    print("      V       %s" % q(tt[:, 1] - tt[:, 6]))
                     print("    chunks    %s" % q(tt[:, 2] - tt[:, 1]))
                     print("    epilogue  %s" % q(tt[:, 3] - tt[:, 2]))
                     print("    tail      %s" % q(tt[:, 7] - tt[:, 3]))
