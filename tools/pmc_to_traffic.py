@@ -21,7 +21,7 @@ import json
 import sys
 
 NAMES = {"pass_kernel<%d, 0>": "pass_a", "upd_kernel<%d, false>": "fin",
-         "gm_kernel<%d>": "gene",  # (large-K X rows + S partials: the gene label)
+         "gm_kernel<%d, 1>": "gene", "gm_kernel<%d, 2>": "gene",  # (large-K X rows + S partials)
          # small-K kernels (csrc/sk.h), labelled as EMEngine.LABELS names them
          "sky_pass_kernel<%d>": "fused", "sk_pass_kernel<%d, 3>": "fused", "sk_pass_kernel<%d, 0>": "pass_a",
          "sk_pass_kernel<%d, 2>": "pass_b", "sk_fin_kernel<%d, false>": "fin"}
@@ -50,7 +50,7 @@ def main(root, K, E_obs, B, out):
            "l2_fabric_bytes_per_launch": {}, "fetch_doubled": {}, "tcc_hit_rate": {}, "counters": {}}
     for pat, key in NAMES.items():
         cs = acc.get(pat % K)
-        if not cs:
+        if not cs or key in rec["counters"]:
             continue
         mean = {c: sum(v) / len(v) for c, v in cs.items()}
         rec["counters"][key] = mean
