@@ -96,8 +96,10 @@ def spawn_ranks(n):
 KERNEL_NAMES = {"pass_a": "pass_kernel<%d, PASS_A> (stream 0: V, Z, Z', d, c, the j / k Y entries, M0 "
                           "partial rows; FP64 MFMA)",
                 "gene": "gm_kernel<%d> (X rows and S partials from the M0 partial rows, FP64 MFMA)",
-                "fused": "fused E-step: sky_pass_kernel<%d> (SK_Y, stream 0: V, Z, Z', d, c, Y entries, "
-                         "M, X, S partials) / sk_pass_kernel<K, SK_U> (3 streams); FP64 MFMA",
+                "fused": "fused E-step: sk_pass_kernel<%d, SK_U> (all three streams: V, Z, d, c, M, X; "
+                         "stream 0 also the S partials); FP64 MFMA",
+                "fused_sky": "fused E-step: sky_pass_kernel<%d> (SK_Y, stream 0: V, Z, Z', d, c, Y entries, "
+                             "M, X, S partials); FP64 MFMA",
                 "pass_b": "sk_pass_kernel<%d, SK_B> (streams 1/2: M1, M2, X)",
                 "fin": "fin: sk_fin_kernel<%d> / upd_kernel (theta and p update)"}
 
@@ -242,7 +244,8 @@ def roofline_record(K, P, R, B, E_obs, plan, iter_s, b2b, build_id):
             "hbm": {"bytes_per_iteration": b8, "achieved": b8 / iter_s / 1e9, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": b8 / iter_s / 1e9 / HBM_PEAK_GBS,
                     "traffic_over_compulsory": None if traffic is None else traffic / b8},
-            "dominant_kernel": {"kernel": KERNEL_NAMES[dom] % K, "avg_launch_us": dom_s * 1e6,
+            "dominant_kernel": {"kernel": KERNEL_NAMES["fused_sky" if dom == "fused" and plan.get("small_k") == 3
+                                                    else dom] % K, "avg_launch_us": dom_s * 1e6,
                                 "executed_flops_per_launch": dfl, "algorithmic_bytes_per_launch": dby,
                                 "tflops": dfl / dom_s / 1e12, "mfma_frac": dfl / dom_s / 1e12 / FP64_PEAK_TFLOPS,
                                 "gbs": dby / dom_s / 1e9, "hbm_frac": dby / dom_s / 1e9 / HBM_PEAK_GBS,
