@@ -159,7 +159,10 @@ class _FileModel:
         return M()
 
 
-def _ranked_worker(rank, world, port, argv, queue, pid=None):
+def _ranked_worker(rank, world, port, argv, queue, pid=None, dump_s=None):
+    import faulthandler
+    if dump_s:  # a rank still running near the parent's deadline prints where it is (stderr)
+        faulthandler.dump_traceback_later(dump_s)
     import torch.distributed as dist  # noqa: F401
     from oracle_engine import OracleEngine
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
@@ -178,6 +181,31 @@ def _ranked_worker(rank, world, port, argv, queue, pid=None):
                       out=lines.append,
                       engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links, B=n))
     queue.put((rank, rc, lines))
+
+
+def _run_ranks(world, argv, timeout, pid=None):
+    """`world` gloo ranks of cli.main (spawned processes) -> {rank: (rc, lines)}; ranks still alive
+    when the results are in (or when collecting them fails) are terminated, so a failing test leaves
+    no process behind."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()  # (a pid-derived port collided with another xdist worker's test)
+    procs = [ctx.Process(target=_ranked_worker, args=(r, world, port, argv, q, pid, timeout - 20))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = {r: (rc, lines) for r, rc, lines in (q.get(timeout=timeout) for _ in procs)}
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+        return got
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+                p.join(10)
 
 
 def _pool_run(argv, out_dir, engines=None):
@@ -238,7 +266,6 @@ def test_two_rank_gloo_cli_writes_the_one_rank_files(tmp_path):
     rank over 16 samples: the Sample_<n>_K<k>.csv files are byte-identical to a one-process
     `--batch 4` run's, and rank 0 prints every sample's summary line in sample order (VERDICT r3
     item 5, r4 item 2; src/run.sh:36-45, :1253-1279)."""
-    import multiprocessing as mp
 
     from oracle_engine import OracleEngine
     one, two = tmp_path / "one", tmp_path / "two"
@@ -257,17 +284,7 @@ def test_two_rank_gloo_cli_writes_the_one_rank_files(tmp_path):
         rc = cli.main(base + ["-o", str(one) + os.sep], model_factory=factory, out=lines1.append,
                       engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links, B=n))
     assert rc == 0
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()  # (a pid-derived port collided with another xdist worker's test)
-    argv = base + ["-o", str(two) + os.sep]
-    procs = [ctx.Process(target=_ranked_worker, args=(r, 2, port, argv, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    got = {r: (rc, lines) for r, rc, lines in (q.get(timeout=240) for _ in procs)}
-    for p in procs:
-        p.join(60)
-        assert p.exitcode == 0
+    got = _run_ranks(2, base + ["-o", str(two) + os.sep], 240)
     assert got[0][0] == 0 and got[1][0] == 0
     assert got[1][1] == []                                   # rank 1 prints nothing
     files1, files2 = sorted(os.listdir(one)), sorted(os.listdir(two))
@@ -288,24 +305,13 @@ def test_gpus_flag_validation():
 def test_two_ranks_without_seed_replay_rank0_stream(tmp_path):
     """ADVICE r4: under an external launcher a rank given no --seed seeds from its own pid (:1149);
     the ranks take rank 0's seed, so the files equal a one-process run seeded with it."""
-    import multiprocessing as mp
     one, two = tmp_path / "one", tmp_path / "two"
     one.mkdir()
     two.mkdir()
     base = ["-k", "2", "-i", "40", "-n", "6", "-f", "3", "-b", "4", "-t", TRAIN, "-e", TEST, "--batch", "2"]
     rc, lines1 = _pool_run(base + ["--seed", "4100"], one)
     assert rc == 0
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=_ranked_worker, args=(r, 2, port, base + ["-o", str(two) + os.sep], q, 4100))
-             for r in range(2)]
-    for p in procs:
-        p.start()
-    got = {r: (rc, lines) for r, rc, lines in (q.get(timeout=240) for _ in procs)}
-    for p in procs:
-        p.join(60)
-        assert p.exitcode == 0
+    got = _run_ranks(2, base + ["-o", str(two) + os.sep], 240, pid=4100)
     assert got[0][0] == 0 and got[1][0] == 0
     files = sorted(os.listdir(one))
     assert files and files == sorted(os.listdir(two))
@@ -342,7 +348,6 @@ def test_eight_rank_gloo_cli_config3_topology(tmp_path):
     the reference's check schedule / convergence rule (:1262-1279).  The Sample files equal a
     one-process `--batch 8` run's byte for byte, rank 0's gathered summary lists all 64 samples
     in sample order, and the other ranks print nothing (src/run.sh:36-45, :1253-1279)."""
-    import multiprocessing as mp
     one, eight = tmp_path / "one", tmp_path / "eight"
     one.mkdir()
     eight.mkdir()
@@ -350,17 +355,7 @@ def test_eight_rank_gloo_cli_config3_topology(tmp_path):
             "--batch", "8"]
     rc, lines1 = _pool_run(base, one)
     assert rc == 0
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
-    argv = base + ["-o", str(eight) + os.sep]
-    procs = [ctx.Process(target=_ranked_worker, args=(r, 8, port, argv, q)) for r in range(8)]
-    for p in procs:
-        p.start()
-    got = {r: (rc, lines) for r, rc, lines in (q.get(timeout=400) for _ in procs)}
-    for p in procs:
-        p.join(60)
-        assert p.exitcode == 0
+    got = _run_ranks(8, base + ["-o", str(eight) + os.sep], 400)
     assert all(got[r][0] == 0 for r in range(8))
     assert all(got[r][1] == [] for r in range(1, 8))
     summary = lambda ls: [l for l in ls if l.startswith("Sample ") and "iterations" in l]  # noqa: E731

@@ -1930,12 +1930,24 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
   // gm_kernel (round 5): 128 rows (two 64-row tiles) per part, at most 1,024 parts per rating
   // (longer parts beyond that: gm_kernel walks any number of 64-row tiles), so the S partials take
   // at most R x 1,024 x K^3 doubles per sample whatever E (2 x 1,024 x 27,000 x 8 B = 442 MB at K=30)
+  // Round 6: a link set whose 128-row parts number fewer than the device's CUs (a fold0-sized set:
+  // 32 parts at K = 20) takes 64-row parts (one row tile each), twice the gm_kernel workgroups:
+  // one sample at K = 13-32 +12-28 %, 8 samples -1-2 % (profiles/r06sp_rows64_ab.txt).  The rule
+  // reads the links and the CU count alone, never B, so a sample's bits do not depend on its batch.
   int sp_rows = c->K <= 12 ? 16 : 128;
-  if (const char* e = getenv("MMSBM_SP_ROWS")) sp_rows = std::max(4, atoi(e));
+  const char* sp_env = getenv("MMSBM_SP_ROWS");
+  if (sp_env) sp_rows = std::max(4, atoi(sp_env));
   const int sp_cap = c->sk ? 256 : 1024;
-  sd.h = mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b,
-                           c->gcap, sp_rows, c->sk, 1024, c->sk_fused,
-                           mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge, sp_cap, pnw_host(c->K));
+  auto build_plan = [&]() {
+    return mmsbm_plan::build(ids_host, counts_host, E, c->R, c->P, em, units_a, units_b, c->gcap, sp_rows,
+                             c->sk, 1024, c->sk_fused, mmsbm_plan::sk_gu(c->K), rho, c->sk_y, balance, merge,
+                             sp_cap, pnw_host(c->K));
+  };
+  sd.h = build_plan();
+  if (em && !c->sk && !sp_env && sd.h.n_sp < c->ncu) {
+    sp_rows = 64;
+    sd.h = build_plan();
+  }
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
   sd.unit_target = c->sk_fused ? units_a : 0;
