@@ -585,36 +585,51 @@ def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
     np.testing.assert_allclose(m.compute_likelihood("test"), LT_o, rtol=RTOL)
 
 
+def _gm_valid_cs(K):
+    """GM<K>::cs_ok: workgroups per S part that divide the NQ fixed X groups of QC chunks (up to
+    four at K = 17-24, two at K <= 16 and K >= 25) and keep one workgroup's S accumulators within
+    8 chunks (csrc/mmsbm.hip GM)."""
+    nch = (K * K + 63) // 64
+    qc = (nch + 1) // 2 if (K <= 16 or K >= 25) else (nch + 3) // 4
+    nq = (nch + qc - 1) // qc
+    return [cs for cs in range(1, nq + 1) if nq % cs == 0 and (cs > 1 or nch <= 8) and (nq // cs) * qc <= 8]
+
+
 @pytest.mark.parametrize("K", [13, 16, 20, 22])
 def test_gm_workgroups_per_part_keep_bits(tmp_path, monkeypatch, K):
-    """gm_kernel forms its X rows in two fixed halves of the cell chunks (GM<K>::HALF), so one or
-    two workgroups per S part (MMSBM_GM_CS=1 / 2) give the same bits: the launch may follow the
-    batch.  Both agree bit for bit and with the C oracle."""
+    """gm_kernel forms its X rows in NQ fixed groups of the cell chunks (GM<K>::NQ: up to four at
+    K = 17-24, two at K <= 16 and K >= 25), so every valid count of workgroups per S part (MMSBM_GM_CS = 1, 2, 3,
+    4 as GM<K> allows) gives the same bits: the launch may follow the batch.
+    All agree bit for bit and with the C oracle."""
     tr, te = _fold(tmp_path, 150, 2500, seed=K + 40, multi_frac=0.05, both_frac=0.02)
+    valid = _gm_valid_cs(K)
+    assert len(valid) >= 2, valid
     out = {}
-    for cs in ("1", "2"):
-        monkeypatch.setenv("MMSBM_GM_CS", cs)
+    for cs in valid:
+        monkeypatch.setenv("MMSBM_GM_CS", str(cs))
         m = _gpu_model(tr, te)
         random.seed(K)
         m.initialize_parameters(K)
         theta0, pr0 = np.array(m.theta), np.array(m.pr)
         m.make_iterations(2)
-        assert m._engine.plan_info()["gm_groups"] == int(cs)
+        assert m._engine.plan_info()["gm_groups"] == cs
         out[cs] = (np.array(m.theta), np.array(m.pr), m.compute_likelihood("train"))
-    np.testing.assert_array_equal(out["1"][0], out["2"][0])
-    np.testing.assert_array_equal(out["1"][1], out["2"][1])
-    assert out["1"][2] == out["2"][2]
+    ref = out[valid[0]]
+    for cs in valid[1:]:
+        np.testing.assert_array_equal(out[cs][0], ref[0])
+        np.testing.assert_array_equal(out[cs][1], ref[1])
+        assert out[cs][2] == ref[2]
     th_o, pr_o, L_o, _ = _oracle_run(m, theta0, pr0, 2)
-    np.testing.assert_allclose(out["1"][0], th_o, rtol=RTOL, atol=ATOL)
-    np.testing.assert_allclose(out["1"][1], pr_o, rtol=RTOL, atol=ATOL)
-    np.testing.assert_allclose(out["1"][2], L_o, rtol=RTOL)
+    np.testing.assert_allclose(ref[0], th_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(ref[1], pr_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(ref[2], L_o, rtol=RTOL)
 
 
 def test_gm_workgroups_follow_the_batch_with_the_same_bits(tmp_path, monkeypatch):
-    """Without the override gm_kernel takes two workgroups per S part where the doubled grid fits
-    one round of resident workgroups (one sample) and one where it would not (8 samples): a
+    """Without the override gm_kernel takes the most workgroups per S part whose grid fits one
+    round of resident workgroups (one sample: four) and one where none would (8 samples): a
     sample run alone and the same sample in slot 3 of an 8-sample engine end bit for bit equal
-    (K=20, ~19 parts)."""
+    (K=20, ~38 parts of 64 rows)."""
     from trigenicinteractionpredictor_amd import EMEngine
     from trigenicinteractionpredictor_amd.layout import links_to_arrays
     monkeypatch.delenv("MMSBM_GM_CS", raising=False)
@@ -637,7 +652,7 @@ def test_gm_workgroups_follow_the_batch_with_the_same_bits(tmp_path, monkeypatch
     g8, g1 = big.plan_info()["gm_groups"], one.plan_info()["gm_groups"]
     import torch
     if torch.cuda.get_device_properties(big.device).multi_processor_count == 256:  # (the rule counts CUs)
-        assert (g8, g1) == (1, 2), (g8, g1)
+        assert (g8, g1) == (1, 4), (g8, g1)
     big.iterate(2)
     one.iterate(2)
     tb, pb = big.download()

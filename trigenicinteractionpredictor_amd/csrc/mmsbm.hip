@@ -801,14 +801,26 @@ struct GM {
   static constexpr int AP = 16 * NA;
   static constexpr int RT = 64, CW = 64;     // rows per row tile, cells per chunk
   static constexpr int NCH = (K2 + CW - 1) / CW;
-  // X rows in two halves of the chunks, [0, HALF) and [HALF, NCH), whatever the launch (round 6):
-  // a part's cells run as one workgroup (CS = 1, both halves in one) or two (CS = 2, one half
-  // each) with the same bits, so the launch can choose CS per batch (upd adds the halves in order)
-  static constexpr int HALF = (NCH + 1) / 2;
-  static constexpr int NH = NCH > 1 ? 2 : 1;               // X-row halves
+  // X rows in NQ fixed groups of QC chunks ([j QC, min((j + 1) QC, NCH))), whatever the launch
+  // (round 6): a part's cells run as CS workgroups of NQ / CS consecutive groups each (CS = 1, 2 when
+  // NQ is even, NQ) with the same bits, so the launch can choose CS per batch (upd adds the groups
+  // in order).  Up to four groups at K = 17-24 (one wave forms a whole X tile, written at the
+  // group's last chunk); two at K <= 16, where two waves split each tile's k-steps and add their
+  // parts through LDS after the row tile's chunks (two groups' parts fit the freed M tile), and at
+  // K >= MMSBM_LDS_BIG (XPOST below)
+  // X rows written after a row tile's chunks (two groups) where two waves split an X tile's k-steps
+  // (K <= 16) or where one workgroup's S accumulators fill the registers (K >= MMSBM_LDS_BIG: a group
+  // written at its last chunk cost K = 30 eight spilled VGPRs, 0.7 %); else at each group's last chunk
+  static constexpr bool XPOST = 8 / (4 * NA) == 2 || K >= MMSBM_LDS_BIG;
+  static constexpr int QC = XPOST ? (NCH + 1) / 2 : (NCH + 3) / 4;  // chunks per X group
+  static constexpr int NQ = (NCH + QC - 1) / QC;          // X groups (all non-empty)
   static constexpr bool ONE = NCH <= 8;                   // CS = 1 possible (its S accumulators fit)
+  static constexpr bool cs_ok(int cs) {                   // a valid workgroups-per-part count
+    return cs >= 1 && cs <= NQ && NQ % cs == 0 && (cs > 1 || ONE) && (NQ / cs) * QC <= 8;
+  }
   static constexpr int TST = AP == 32 ? 48 : 16;  // theta tile row stride (= 16 mod 32 doubles)
   static constexpr int XT = 4 * NA, XK = 8 / XT;  // X tiles per row tile, k-splits per tile
+  static constexpr int NXR = NQ;                  // X row sets (one per group)
   static constexpr int ST = 4 * NA, SK = 8 / ST;  // S tiles per chunk, row splits per tile
   static constexpr int MW = K2 % 2 == 0 ? 2 : 1;  // staging width (a row starts 16-B aligned)
   static constexpr int NM = RT * CW / MW / 512;   // M staging loads per thread
@@ -819,6 +831,15 @@ struct GM {
   static_assert(XT * XK == 8 && ST * SK == 8, "gm: 8 waves");
   static_assert(RT * CW % (MW * 512) == 0 && RT * AP % 512 == 0, "gm staging");
 };
+
+// host view of GM<K>::NXR (the X row sets gm_kernel writes)
+constexpr int gm_nxr(int K) {
+  const int nch = (K * K + 63) / 64, xk = 8 / (4 * ((K + 15) / 16));
+  const int qc = (xk == 2 || K >= MMSBM_LDS_BIG) ? (nch + 1) / 2 : (nch + 3) / 4;
+  return (nch + qc - 1) / qc;
+}
+static_assert(gm_nxr(30) == GM<30>::NXR && gm_nxr(16) == GM<16>::NXR && gm_nxr(13) == GM<13>::NXR &&
+                  gm_nxr(20) == GM<20>::NXR && gm_nxr(24) == GM<24>::NXR && gm_nxr(25) == GM<25>::NXR, "gm_nxr");
 
 // column swizzle of the 64-wide LDS tiles: bit 4 <- row bit 0, bits 1-3 <- row bits 1-3
 __device__ __forceinline__ int gm_swz(int r) { return ((r & 1) << 4) | (((r >> 1) & 7) << 1); }
@@ -838,17 +859,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
   double* Tl = Pt + AP * CW;         // [RT][TST]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int CPG = CS == 2 ? G::HALF : G::NCH;  // chunks of this workgroup's group
-  constexpr int NXH = CS == 2 ? 1 : G::NH;          // X halves this workgroup forms
+  static_assert(G::cs_ok(CS), "gm_kernel: workgroups per part");
+  constexpr int NXH = G::NQ / CS;                   // X groups this workgroup forms
+  constexpr int CPG = NXH * G::QC;                  // its chunks (the last workgroup's may end early)
+  constexpr int QC = G::QC;
   const int w = blockIdx.x / CS, grp = blockIdx.x % CS, b = blockIdx.y;
-  const int cb = grp * G::HALF;      // the group's first chunk (0 for CS = 1)
+  const int cb = grp * CPG;          // its first chunk (0 for CS = 1)
   const int l15 = lane & 15, l4 = lane >> 4;
   const int* d = sp_desc + 3 * w;
   const int r = d[0], q0 = d[1], q1 = d[2];
   const double* __restrict__ th = theta + (size_t)b * P * K;
   const double* __restrict__ p = pr + ((size_t)b * R + r) * K3;
   const double* __restrict__ mb = prows + (size_t)b * n_prows * K2;
-  double* __restrict__ xb = xrow + (size_t)grp * xgs + (size_t)b * n_prows * K;  // xgs: one half's X rows
+  double* __restrict__ xb = xrow + (size_t)b * n_prows * K;  // xgs: one group's X rows
   // this wave's X tile (row tile xr, a tile xa, k-split xk) and S tile (cell tile sc, a tile sa,
   // row split sk) of every chunk
   const int xt = wv % G::XT, xk = wv / G::XT, xr = xt % 4, xa = xt / 4;
@@ -927,10 +950,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
     load_m(q0, cb, mv);
     load_p(cb, pv);
   }
+  constexpr bool XPOST = G::XPOST;
+  constexpr int NXA = XPOST ? NXH : 1;  // X accumulators held over the row tile's chunks
   for (int qt = q0; qt < q1; qt += RT) {
-    d4v xacc[NXH];
+    d4v xacc[NXA];
 #pragma unroll
-    for (int j = 0; j < NXH; ++j) xacc[j] = d4v{0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < NXA; ++j) xacc[j] = d4v{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int i = 0; i < CPG; ++i) {
       const int c = cb + i;
@@ -948,12 +973,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
         load_p(cb, pv);
         load_t(qt + RT, tv);
       }
-      // X tile: rows 16 xr + i, a 16 xa + j; k = the chunk's cells, into the chunk's half
-      const int hx = (CS == 2 || i < G::HALF) ? 0 : 1;  // (compile-time: i is unrolled, cb = 0 for CS = 1)
+      // X tile: rows 16 xr + i, a 16 xa + j; k = the chunk's cells (this wave's k-split of them)
+      const int hx = XPOST ? i / QC : 0;  // (compile-time: i is unrolled, cb a multiple of QC)
 #pragma unroll 4
       for (int s = xk * XKS; s < (xk + 1) * XKS; ++s) {
         const int cell = 4 * s + l4;
         xacc[hx] = mfma16(xm[cell ^ xsw_m], xp[cell ^ xsw_p], xacc[hx]);
+      }
+      // K > 16: the chunk ends its X group (QC chunks; the part's last chunk ends the last group),
+      // whose X rows go out at once (no register holds a group past its chunks)
+      if constexpr (!XPOST) {
+        constexpr int ILAST = (G::NCH - 1) - (CS - 1) * CPG;  // the part's last chunk, in the last workgroup
+        if (i % QC == QC - 1 || (i == ILAST && grp == CS - 1)) {  // (uniform; i is compile-time)
+          const int xs = grp * NXH + i / QC;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = 16 * xr + l4 + 4 * e, a = 16 * xa + l15;
+            if (qt + row < q1 && a < K) xb[xs * xgs + (size_t)(qt + row) * K + a] = xacc[0][e];
+          }
+          xacc[0] = d4v{0.0, 0.0, 0.0, 0.0};
+        }
       }
       // S tile: a 16 sa + i, cells 16 sc + j of the chunk; k = the tile's rows
 #pragma unroll 4
@@ -962,31 +1001,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
         sacc[i] = mfma16(sT[row * TST], Ml[row * CW + (scell ^ gm_swz(row))], sacc[i]);
       }
     }
-    // X rows of this tile, per half: the k-splits' parts added in wave order (XK = 2: through LDS)
-    if constexpr (G::XK == 1) {
+    if constexpr (XPOST && G::XK == 1) {
 #pragma unroll
       for (int j = 0; j < NXH; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 16 * xr + l4 + 4 * i, a = 16 * xa + l15;
-          if (qt + row < q1 && a < K) xb[j * xgs + (size_t)(qt + row) * K + a] = xacc[j][i];
+        for (int e = 0; e < 4; ++e) {
+          const int row = 16 * xr + l4 + 4 * e, a = 16 * xa + l15;
+          if (qt + row < q1 && a < K) xb[(grp * NXH + j) * xgs + (size_t)(qt + row) * K + a] = xacc[j][e];
         }
-    } else {
-      __syncthreads();  // Ml is free: park split 1's parts there (half j at 2048 j)
+    }
+    if constexpr (G::XK == 2) {
+      // K <= 16: the row tile's X rows per group, the k-splits' parts added in wave order through
+      // LDS (Ml is free: group j's parts at 2048 j)
+      static_assert(NXH <= 2, "two groups' parts in the M tile");
+      __syncthreads();
       if (xk == 1)
 #pragma unroll
         for (int j = 0; j < NXH; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) Ml[2048 * j + (xt * 4 + i) * 64 + lane] = xacc[j][i];
+          for (int e = 0; e < 4; ++e) Ml[2048 * j + (xt * 4 + e) * 64 + lane] = xacc[j][e];
       __syncthreads();
       if (xk == 0)
 #pragma unroll
         for (int j = 0; j < NXH; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int row = 16 * xr + l4 + 4 * i, a = 16 * xa + l15;
-            const double v = xacc[j][i] + Ml[2048 * j + (xt * 4 + i) * 64 + lane];
-            if (qt + row < q1 && a < K) xb[j * xgs + (size_t)(qt + row) * K + a] = v;
+          for (int e = 0; e < 4; ++e) {
+            const int row = 16 * xr + l4 + 4 * e, a = 16 * xa + l15;
+            const double v = xacc[j][e] + Ml[2048 * j + (xt * 4 + e) * 64 + lane];
+            if (qt + row < q1 && a < K) xb[(grp * NXH + j) * xgs + (size_t)(qt + row) * K + a] = v;
           }
     }
   }
@@ -1063,7 +1105,7 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
       for (int q = prow_ptr[(size_t)r * (P + 1) + g], qe = prow_ptr[(size_t)r * (P + 1) + g + 1]; q < qe; ++q) {
         double x = xb[(size_t)q * K];
 #pragma unroll
-        for (int h = 1; h < GM<K>::NH; ++h) x += xb[h * xgs + (size_t)q * K];
+        for (int h = 1; h < GM<K>::NXR; ++h) x += xb[h * xgs + (size_t)q * K];
         X += x;
       }
     constexpr int YS = y_stride(K), EPI = 128 / YS, WW = EPI * YS, LW = WW / 2, YU2 = 8;
@@ -1376,7 +1418,7 @@ struct mmsbm_ctx {
   bool warm = false;                 // a direct iteration ran (LDS opt-ins done before capture)
   hipStream_t cap = nullptr;         // capture stream (torch's default stream cannot be captured)
   hipGraphExec_t gexec = nullptr;
-  double* xrows = nullptr;       // gm_kernel's X rows [2 halves][B][n_prows][K]
+  double* xrows = nullptr;       // gm_kernel's X rows [GM<K>::NXR groups][B][n_prows][K]
   int ncu = 256;                 // the device's compute units (gm_kernel's split rule)
   int gm_cs = 0;                 // MMSBM_GM_CS: force gm_kernel's workgroups per part (0: by batch)
   const double *g_theta = nullptr, *g_pr = nullptr;
@@ -1433,8 +1475,8 @@ WsLayout ws_layout(const mmsbm_ctx* c) {
   off += align_up(B * (size_t)c->P * c->K * 8);
   L.S = off;
   off += align_up(B * c->R * K3 * 8);
-  L.xrows = off;  // gm_kernel's X rows: two halves (GM<K>::NH)
-  off += align_up(2 * B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
+  L.xrows = off;  // gm_kernel's X row groups (GM<K>::NXR <= 4)
+  off += align_up(gm_nxr(c->K) * B * std::max<long long>(tr.n_prows, 1) * c->K * 8);
   L.total = off;
   return L;
 }
@@ -1463,19 +1505,37 @@ int lds_opt_in(mmsbm_ctx* c, unsigned bit, KernelT* kern, int bytes) {
   return MMSBM_OK;
 }
 
-// gm_kernel's workgroups per part (the bits are the same either way, GM<K>::HALF): two where the
-// doubled grid still fits one round of resident workgroups (one sample at K = 13-22: the grid is a
-// few dozen parts; r05: K=20 +24 %, K=16 +13.5 %), one where it would not (K=20 x 8: -6 % with
-// two); two always where one workgroup's S accumulators would not fit (NCH > 8); one for a single
-// chunk.  MMSBM_GM_CS=1/2 forces it where both exist (tests, measurement).
+// gm_kernel's workgroups per part, CS (the bits are the same for every valid CS: GM<K>::NQ fixed X
+// groups): the largest valid CS whose grid still fits one round of resident workgroups (one sample
+// at K = 13-32: the grid is a few dozen to a few hundred parts; r05: two per part at K=20 +24 %),
+// else the smallest valid one (K=20 x 8: -6 % with two; one is invalid where one workgroup's S
+// accumulators would not fit, NCH > 8).  MMSBM_GM_CS=n forces a valid n (tests, measurement).
 template <int K>
 int gm_cs(const mmsbm_ctx* c, int nsp) {
   using G = GM<K>;
-  if (!G::ONE) return 2;
-  if (G::NCH == 1) return 1;
-  if (c->gm_cs == 1 || c->gm_cs == 2) return c->gm_cs;
+  if (c->gm_cs > 0 && G::cs_ok(c->gm_cs)) return c->gm_cs;
   const long long slots = (long long)c->ncu * (G::WPE >= 4 ? 2 : 1);
-  return 2LL * nsp * nb_of(c) <= slots ? 2 : 1;
+  int lo = 0, best = 0;
+  for (int cs = 1; cs <= G::NQ; ++cs) {
+    if (!G::cs_ok(cs)) continue;
+    if (!lo) lo = cs;
+    if ((long long)cs * nsp * nb_of(c) <= slots) best = cs;
+  }
+  return best ? best : lo;
+}
+
+// one gm_kernel launch with CS workgroups per part (a CS GM<K> does not allow is never chosen)
+template <int K, int CS>
+int launch_gm(mmsbm_ctx* c, const SetDev& sd, int nsp, const double* theta, const double* pr,
+              hipStream_t s) {
+  if constexpr (GM<K>::cs_ok(CS)) {
+    int rc;
+    if ((rc = lds_opt_in(c, 9 + CS, &gm_kernel<K, CS>, GM<K>::LDS))) return rc;
+    gm_kernel<K, CS><<<dim3(CS * nsp, nb_of(c)), 512, GM<K>::LDS, s>>>(
+        theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, sd.h.n_prows, nsp,
+        (long long)c->B * sd.h.n_prows * K);
+  }
+  return MMSBM_OK;
 }
 
 template <int K>
@@ -1487,21 +1547,13 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
   int rc;
   if (mode == PASS_B) {  // launch 2: gm_kernel (X rows + S partials in one pass); upd sums Y
     const int nsp = std::max(h.n_sp, 1);
-    if (gm_cs<K>(c, nsp) == 1) {
-      if constexpr (GM<K>::ONE) {
-        if ((rc = lds_opt_in(c, 10, &gm_kernel<K, 1>, GM<K>::LDS))) return rc;
-        gm_kernel<K, 1><<<dim3(nsp, nb_of(c)), 512, GM<K>::LDS, s>>>(
-            theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, h.n_prows, nsp,
-            (long long)c->B * h.n_prows * K);
-      }
-    } else {
-      if constexpr (GM<K>::NCH > 1) {
-        if ((rc = lds_opt_in(c, 11, &gm_kernel<K, 2>, GM<K>::LDS))) return rc;
-        gm_kernel<K, 2><<<dim3(2 * nsp, nb_of(c)), 512, GM<K>::LDS, s>>>(
-            theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, h.n_prows, nsp,
-            (long long)c->B * h.n_prows * K);
-      }
+    switch (gm_cs<K>(c, nsp)) {
+      case 1: rc = launch_gm<K, 1>(c, sd, nsp, theta, pr, s); break;
+      case 2: rc = launch_gm<K, 2>(c, sd, nsp, theta, pr, s); break;
+      case 3: rc = launch_gm<K, 3>(c, sd, nsp, theta, pr, s); break;
+      default: rc = launch_gm<K, 4>(c, sd, nsp, theta, pr, s); break;
     }
+    if (rc) return rc;
   } else {
     if (h.n_wg_a == 0) return MMSBM_OK;
     // dynamic LDS for the context's gene cap (<= the compile-time GMAX the opt-in covers)
