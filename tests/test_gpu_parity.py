@@ -587,18 +587,18 @@ def test_kernel_family_matches_oracle(tmp_path, monkeypatch, K, env):
 
 def _gm_valid_cs(K):
     """GM<K>::cs_ok: workgroups per S part that divide the NQ fixed X groups of QC chunks (up to
-    four at K = 17-24, two at K <= 16 and K >= 25) and keep one workgroup's S accumulators within
-    8 chunks (csrc/mmsbm.hip GM)."""
+    four above K = 16 -- at K >= 25 on plans with fewer parts than CUs, like these -- two at
+    K <= 16) and keep one workgroup's S accumulators within 8 chunks (csrc/mmsbm.hip GM)."""
     nch = (K * K + 63) // 64
-    qc = (nch + 1) // 2 if (K <= 16 or K >= 25) else (nch + 3) // 4
+    qc = (nch + 1) // 2 if K <= 16 else (nch + 3) // 4  # (K >= 25: these small plans take GM::Q4)
     nq = (nch + qc - 1) // qc
     return [cs for cs in range(1, nq + 1) if nq % cs == 0 and (cs > 1 or nch <= 8) and (nq // cs) * qc <= 8]
 
 
-@pytest.mark.parametrize("K", [13, 16, 20, 22])
+@pytest.mark.parametrize("K", [13, 16, 20, 22, 30])
 def test_gm_workgroups_per_part_keep_bits(tmp_path, monkeypatch, K):
-    """gm_kernel forms its X rows in NQ fixed groups of the cell chunks (GM<K>::NQ: up to four at
-    K = 17-24, two at K <= 16 and K >= 25), so every valid count of workgroups per S part (MMSBM_GM_CS = 1, 2, 3,
+    """gm_kernel forms its X rows in NQ fixed groups of the cell chunks (up to four above K = 16,
+    at K >= 25 on small plans (GM::Q4), two at K <= 16), so every valid count of workgroups per S part (MMSBM_GM_CS = 1, 2, 3,
     4 as GM<K> allows) gives the same bits: the launch may follow the batch.
     All agree bit for bit and with the C oracle."""
     tr, te = _fold(tmp_path, 150, 2500, seed=K + 40, multi_frac=0.05, both_frac=0.02)

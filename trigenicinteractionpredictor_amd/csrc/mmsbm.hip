@@ -814,13 +814,20 @@ struct GM {
   static constexpr bool XPOST = 8 / (4 * NA) == 2 || K >= MMSBM_LDS_BIG;
   static constexpr int QC = XPOST ? (NCH + 1) / 2 : (NCH + 3) / 4;  // chunks per X group
   static constexpr int NQ = (NCH + QC - 1) / QC;          // X groups (all non-empty)
+  // Q4 (K >= MMSBM_LDS_BIG, plans with fewer parts than CUs, SetDev::gm_q4): the four-group layout
+  // of K = 17-24 there too (written at each group's last chunk; its CS = 2 form spills, but such
+  // plans run four workgroups per part)
+  static constexpr bool Q4OK = K >= MMSBM_LDS_BIG && 8 / (4 * NA) == 1;
+  static constexpr int QC4 = (NCH + 3) / 4, NQ4 = (NCH + QC4 - 1) / QC4;
+  static constexpr int qc(bool q4) { return q4 && Q4OK ? QC4 : QC; }
+  static constexpr int nq(bool q4) { return q4 && Q4OK ? NQ4 : NQ; }
   static constexpr bool ONE = NCH <= 8;                   // CS = 1 possible (its S accumulators fit)
-  static constexpr bool cs_ok(int cs) {                   // a valid workgroups-per-part count
-    return cs >= 1 && cs <= NQ && NQ % cs == 0 && (cs > 1 || ONE) && (NQ / cs) * QC <= 8;
+  static constexpr bool cs_ok(int cs, bool q4 = false) {  // a valid workgroups-per-part count
+    return cs >= 1 && cs <= nq(q4) && nq(q4) % cs == 0 && (cs > 1 || ONE) && (nq(q4) / cs) * qc(q4) <= 8;
   }
   static constexpr int TST = AP == 32 ? 48 : 16;  // theta tile row stride (= 16 mod 32 doubles)
   static constexpr int XT = 4 * NA, XK = 8 / XT;  // X tiles per row tile, k-splits per tile
-  static constexpr int NXR = NQ;                  // X row sets (one per group)
+  static constexpr int NXR = NQ;                  // X row sets (one per group; nq(true) under Q4)
   static constexpr int ST = 4 * NA, SK = 8 / ST;  // S tiles per chunk, row splits per tile
   static constexpr int MW = K2 % 2 == 0 ? 2 : 1;  // staging width (a row starts 16-B aligned)
   static constexpr int NM = RT * CW / MW / 512;   // M staging loads per thread
@@ -833,18 +840,18 @@ struct GM {
 };
 
 // host view of GM<K>::NXR (the X row sets gm_kernel writes)
-constexpr int gm_nxr(int K) {
+constexpr int gm_nxr(int K) {  // (the most of either layout)
   const int nch = (K * K + 63) / 64, xk = 8 / (4 * ((K + 15) / 16));
-  const int qc = (xk == 2 || K >= MMSBM_LDS_BIG) ? (nch + 1) / 2 : (nch + 3) / 4;
+  const int qc = xk == 2 ? (nch + 1) / 2 : (nch + 3) / 4;
   return (nch + qc - 1) / qc;
 }
-static_assert(gm_nxr(30) == GM<30>::NXR && gm_nxr(16) == GM<16>::NXR && gm_nxr(13) == GM<13>::NXR &&
-                  gm_nxr(20) == GM<20>::NXR && gm_nxr(24) == GM<24>::NXR && gm_nxr(25) == GM<25>::NXR, "gm_nxr");
+static_assert(gm_nxr(30) == GM<30>::nq(true) && gm_nxr(16) == GM<16>::NXR && gm_nxr(13) == GM<13>::NXR &&
+                  gm_nxr(20) == GM<20>::NXR && gm_nxr(24) == GM<24>::NXR && gm_nxr(25) == GM<25>::nq(true), "gm_nxr");
 
 // column swizzle of the 64-wide LDS tiles: bit 4 <- row bit 0, bits 1-3 <- row bits 1-3
 __device__ __forceinline__ int gm_swz(int r) { return ((r & 1) << 4) | (((r >> 1) & 7) << 1); }
 
-template <int K, int CS>
+template <int K, int CS, bool Q4 = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE))) void gm_kernel(const double* __restrict__ theta, const double* __restrict__ pr,
                                                   const double* __restrict__ prows,
                                                   const int* __restrict__ prow_gene,
@@ -859,10 +866,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
   double* Tl = Pt + AP * CW;         // [RT][TST]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  static_assert(G::cs_ok(CS), "gm_kernel: workgroups per part");
-  constexpr int NXH = G::NQ / CS;                   // X groups this workgroup forms
-  constexpr int CPG = NXH * G::QC;                  // its chunks (the last workgroup's may end early)
-  constexpr int QC = G::QC;
+  static_assert(G::cs_ok(CS, Q4) && (!Q4 || G::Q4OK), "gm_kernel: workgroups per part");
+  constexpr int NXH = G::nq(Q4) / CS;               // X groups this workgroup forms
+  constexpr int QC = G::qc(Q4);
+  constexpr int CPG = NXH * QC;                     // its chunks (the last workgroup's may end early)
   const int w = blockIdx.x / CS, grp = blockIdx.x % CS, b = blockIdx.y;
   const int cb = grp * CPG;          // its first chunk (0 for CS = 1)
   const int l15 = lane & 15, l4 = lane >> 4;
@@ -950,7 +957,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(GM<K>::WPE)
     load_m(q0, cb, mv);
     load_p(cb, pv);
   }
-  constexpr bool XPOST = G::XPOST;
+  constexpr bool XPOST = G::XPOST && !Q4;
   constexpr int NXA = XPOST ? NXH : 1;  // X accumulators held over the row tile's chunks
   for (int qt = q0; qt < q1; qt += RT) {
     d4v xacc[NXA];
@@ -1078,7 +1085,7 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
     double* __restrict__ S_out, const double* __restrict__ nth_add, const double* __restrict__ q_part,
     double* __restrict__ q_out, int n_qwg, const double* __restrict__ xrow, const int* __restrict__ prow_ptr,
     long long n_prows, long long xgs, const double* __restrict__ ybuf, const int* __restrict__ yptr,
-    long long n_y) {
+    long long n_y, int nxr) {
   constexpr int K2 = K * K, K3 = K * K * K;
   constexpr int NCW = (K3 + 63) / 64, NPART = UPD_NT / 64;
   __shared__ double red[MAX_R * NPART * 64];
@@ -1105,7 +1112,7 @@ __global__ __launch_bounds__(UPD_NT) void upd_kernel(
       for (int q = prow_ptr[(size_t)r * (P + 1) + g], qe = prow_ptr[(size_t)r * (P + 1) + g + 1]; q < qe; ++q) {
         double x = xb[(size_t)q * K];
 #pragma unroll
-        for (int h = 1; h < GM<K>::NXR; ++h) x += xb[h * xgs + (size_t)q * K];
+        for (int h = 1; h < (GM<K>::Q4OK ? nxr : GM<K>::NXR); ++h) x += xb[h * xgs + (size_t)q * K];
         X += x;
       }
     constexpr int YS = y_stride(K), EPI = 128 / YS, WW = EPI * YS, LW = WW / 2, YU2 = 8;
@@ -1352,6 +1359,7 @@ struct SetDev {  // device copy of one link set's plan
   int* skrow12 = nullptr;               // slot-major row12 of group 0
   int ncu = 0;                          // CUs the fused plan's unit target came from (0: none)
   int unit_target = 0;
+  bool gm_q4 = false;                   // K >= MMSBM_LDS_BIG: gm_kernel's four-group X layout (GM<K>::Q4OK)
   void release() {
     void* ps[] = {rows, chunk_prow, chunk_vslot, wg_units, wg_code, wg_gene, vgenes, prow_ptr, prow_gene, sp_desc,
                   row_y, yptr, gptr, sku[0], sku[1], skr[0], skr[1], skrow12};
@@ -1374,7 +1382,7 @@ struct Launch {
   int gmax;
   PassFn sk_pass;  // small-K kernels (sk.h), K <= 12; nullptr above
   FinFn sk_fin;
-  int (*gm_groups)(const mmsbm_ctx*, int);  // gm_kernel's workgroups per part (gm_cs<K>)
+  int (*gm_groups)(const mmsbm_ctx*, int, bool);  // gm_kernel's workgroups per part (gm_cs<K>)
 };
 
 }  // namespace
@@ -1511,13 +1519,14 @@ int lds_opt_in(mmsbm_ctx* c, unsigned bit, KernelT* kern, int bytes) {
 // else the smallest valid one (K=20 x 8: -6 % with two; one is invalid where one workgroup's S
 // accumulators would not fit, NCH > 8).  MMSBM_GM_CS=n forces a valid n (tests, measurement).
 template <int K>
-int gm_cs(const mmsbm_ctx* c, int nsp) {
+int gm_cs(const mmsbm_ctx* c, int nsp, bool q4) {
   using G = GM<K>;
-  if (c->gm_cs > 0 && G::cs_ok(c->gm_cs)) return c->gm_cs;
+  q4 = q4 && G::Q4OK;
+  if (c->gm_cs > 0 && G::cs_ok(c->gm_cs, q4)) return c->gm_cs;
   const long long slots = (long long)c->ncu * (G::WPE >= 4 ? 2 : 1);
   int lo = 0, best = 0;
-  for (int cs = 1; cs <= G::NQ; ++cs) {
-    if (!G::cs_ok(cs)) continue;
+  for (int cs = 1; cs <= G::nq(q4); ++cs) {
+    if (!G::cs_ok(cs, q4)) continue;
     if (!lo) lo = cs;
     if ((long long)cs * nsp * nb_of(c) <= slots) best = cs;
   }
@@ -1525,13 +1534,13 @@ int gm_cs(const mmsbm_ctx* c, int nsp) {
 }
 
 // one gm_kernel launch with CS workgroups per part (a CS GM<K> does not allow is never chosen)
-template <int K, int CS>
+template <int K, int CS, bool Q4>
 int launch_gm(mmsbm_ctx* c, const SetDev& sd, int nsp, const double* theta, const double* pr,
               hipStream_t s) {
-  if constexpr (GM<K>::cs_ok(CS)) {
+  if constexpr (GM<K>::cs_ok(CS, Q4) && (!Q4 || GM<K>::Q4OK)) {
     int rc;
-    if ((rc = lds_opt_in(c, 9 + CS, &gm_kernel<K, CS>, GM<K>::LDS))) return rc;
-    gm_kernel<K, CS><<<dim3(CS * nsp, nb_of(c)), 512, GM<K>::LDS, s>>>(
+    if ((rc = lds_opt_in(c, (Q4 ? 13 : 9) + CS, &gm_kernel<K, CS, Q4>, GM<K>::LDS))) return rc;
+    gm_kernel<K, CS, Q4><<<dim3(CS * nsp, nb_of(c)), 512, GM<K>::LDS, s>>>(
         theta, pr, c->prows, sd.prow_gene, sd.sp_desc, c->xrows, c->spart, c->P, c->R, sd.h.n_prows, nsp,
         (long long)c->B * sd.h.n_prows * K);
   }
@@ -1547,11 +1556,14 @@ int launch_pass(mmsbm_ctx* c, int mode, int which, const double* theta, const do
   int rc;
   if (mode == PASS_B) {  // launch 2: gm_kernel (X rows + S partials in one pass); upd sums Y
     const int nsp = std::max(h.n_sp, 1);
-    switch (gm_cs<K>(c, nsp)) {
-      case 1: rc = launch_gm<K, 1>(c, sd, nsp, theta, pr, s); break;
-      case 2: rc = launch_gm<K, 2>(c, sd, nsp, theta, pr, s); break;
-      case 3: rc = launch_gm<K, 3>(c, sd, nsp, theta, pr, s); break;
-      default: rc = launch_gm<K, 4>(c, sd, nsp, theta, pr, s); break;
+    const bool q4 = sd.gm_q4 && GM<K>::Q4OK;
+    switch (gm_cs<K>(c, nsp, q4) + (q4 ? 4 : 0)) {
+      case 1: rc = launch_gm<K, 1, false>(c, sd, nsp, theta, pr, s); break;
+      case 2: rc = launch_gm<K, 2, false>(c, sd, nsp, theta, pr, s); break;
+      case 3: rc = launch_gm<K, 3, false>(c, sd, nsp, theta, pr, s); break;
+      case 4: rc = launch_gm<K, 4, false>(c, sd, nsp, theta, pr, s); break;
+      case 6: rc = launch_gm<K, 2, true>(c, sd, nsp, theta, pr, s); break;
+      default: rc = launch_gm<K, 4, true>(c, sd, nsp, theta, pr, s); break;
     }
     if (rc) return rc;
   } else {
@@ -1597,12 +1609,12 @@ int launch_fin(mmsbm_ctx* c, bool sums, double* theta, double* pr, double* nth, 
     upd_kernel<K, true><<<dim3(nthw + ncw, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
         nth, S, c->nth_add, nullptr, nullptr, 0, xr, sd.prow_ptr, h.n_prows, (long long)c->B * h.n_prows * K,
-        yb, sd.yptr, h.n_y);
+        yb, sd.yptr, h.n_y, GM<K>::nq(sd.gm_q4));
   else
     upd_kernel<K, false><<<dim3(nthw + ncw + nqc, nb_of(c)), UPD_NT, 0, s>>>(
         theta, pr, c->spart, c->deg, spr, c->P, c->R, std::max(h.n_sp, 1), nthw, c->eps,
         nth, S, c->nth_add, c->q_part, c->q_out, c->n_qwg, xr, sd.prow_ptr, h.n_prows,
-        (long long)c->B * h.n_prows * K, yb, sd.yptr, h.n_y);
+        (long long)c->B * h.n_prows * K, yb, sd.yptr, h.n_y, GM<K>::nq(sd.gm_q4));
   HIP_TRY(hipGetLastError());
   return MMSBM_OK;
 }
@@ -1996,12 +2008,19 @@ int mmsbm_set_links(mmsbm_ctx* c, int32_t which, const int32_t* ids_host, const 
                              sp_cap, pnw_host(c->K));
   };
   sd.h = build_plan();
+  bool small_plan = false;
   if (em && !c->sk && !sp_env && sd.h.n_sp < c->ncu) {
     sp_rows = 64;
     sd.h = build_plan();
+    small_plan = true;
   }
+  // such a plan at K >= MMSBM_LDS_BIG also takes gm_kernel's four-group X layout (GM<K>::Q4OK):
+  // one sample runs four workgroups per part there (MMSBM_GM_Q4=0/1 forces the choice)
+  const char* q4_env = getenv("MMSBM_GM_Q4");
+  const bool gm_q4 = q4_env ? q4_env[0] == '1' : small_plan;
   const auto& h = sd.h;
   sd.ncu = c->sk_fused ? ncu : 0;
+  sd.gm_q4 = em && !c->sk && gm_q4;
   sd.unit_target = c->sk_fused ? units_a : 0;
   if ((rc = upload(&sd.rows, h.rows))) return rc;
   if ((rc = upload(&sd.chunk_prow, h.chunk_prow))) return rc;
@@ -2346,7 +2365,7 @@ int mmsbm_plan_info(const mmsbm_ctx* c, int32_t which, int64_t* info) {
   info[12] = c->sets[which].ncu;
   info[13] = c->sets[which].unit_target;
   info[14] = h.n_y;
-  info[15] = h.small ? 0 : kTable[c->K - 1].gm_groups(c, std::max(h.n_sp, 1));
+  info[15] = h.small ? 0 : kTable[c->K - 1].gm_groups(c, std::max(h.n_sp, 1), c->sets[which].gm_q4);
   return MMSBM_OK;
 }
 
