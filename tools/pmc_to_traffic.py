@@ -21,8 +21,8 @@ import json
 import sys
 
 NAMES = {"pass_kernel<%d, 0>": "pass_a", "upd_kernel<%d, false>": "fin",
-         "gm_kernel<%d, 1>": "gene", "gm_kernel<%d, 2>": "gene", "gm_kernel<%d, 3>": "gene",
-         "gm_kernel<%d, 4>": "gene",  # (large-K X rows + S partials; workgroups per part 1-4)
+         # (large-K X rows + S partials; workgroups per part 1-4, X layout halves / GM::Q4)
+         **{"gm_kernel<%%d, %d%s>" % (cs, q): "gene" for cs in (1, 2, 3, 4) for q in ("", ", false", ", true")},
          # small-K kernels (csrc/sk.h), labelled as EMEngine.LABELS names them
          "sky_pass_kernel<%d>": "fused", "sk_pass_kernel<%d, 3>": "fused", "sk_pass_kernel<%d, 0>": "pass_a",
          "sk_pass_kernel<%d, 2>": "pass_b", "sk_fin_kernel<%d, false>": "fin"}
