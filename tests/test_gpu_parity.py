@@ -166,12 +166,14 @@ def test_work_plan_splits_match_oracle(tmp_path, monkeypatch, K, units):
     (26, 50, 3000, {"MMSBM_SP_ROWS": "8"}),    # many short S-partial parts (gm_kernel row tiles)
     (20, 60, 4000, {"MMSBM_GCAP": "4"}),       # fewer V-table genes per pass-A workgroup
     (20, 60, 4000, {"MMSBM_UNITS": "1,1"}),    # balanced without merging (K < 25)
+    (30, 60, 4000, {"MMSBM_GM_Q4": "0"}),      # a small plan at K >= 25 on gm_kernel's two halves
+    (26, 50, 3000, {"MMSBM_SP_ROWS": "128"}),  # 128-row parts forced on a small plan (no 64-row rule)
 ])
 def test_large_k_plan_variants_match_oracle(tmp_path, monkeypatch, K, P, E, env):
     """The large-K work plans (csrc/plan.h pack_balanced, Plan::merge; mmsbm.hip's merged partial
     rows, gm_kernel's S-partial parts, the pass-A gene cap) with few genes and long pivot runs, so a run's chunks
     spread over several waves of a workgroup, vs the C oracle after 2 iterations."""
-    for k in ("MMSBM_UNITS", "MMSBM_MERGE", "MMSBM_BALANCE", "MMSBM_SP_ROWS", "MMSBM_GCAP"):
+    for k in ("MMSBM_UNITS", "MMSBM_MERGE", "MMSBM_BALANCE", "MMSBM_SP_ROWS", "MMSBM_GCAP", "MMSBM_GM_Q4"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
