@@ -161,6 +161,7 @@ class _FileModel:
 
 def _ranked_worker(rank, world, port, argv, queue, pid=None, dump_s=None):
     import faulthandler
+    faulthandler.enable()  # (a rank that dies on a signal prints where)
     if dump_s:  # a rank still running near the parent's deadline prints where it is (stderr)
         faulthandler.dump_traceback_later(dump_s)
     import torch.distributed as dist  # noqa: F401
@@ -196,7 +197,14 @@ def _run_ranks(world, argv, timeout, pid=None):
     for p in procs:
         p.start()
     try:
-        got = {r: (rc, lines) for r, rc, lines in (q.get(timeout=timeout) for _ in procs)}
+        got = {}
+        for _ in procs:
+            try:
+                r, rc, lines = q.get(timeout=timeout)
+            except Exception as e:  # (which ranks are still running, and how the others ended)
+                states = [(p.pid, p.is_alive(), p.exitcode) for p in procs]
+                raise AssertionError("ranks did not report: %r (pid, alive, exitcode): %r" % (e, states))
+            got[r] = (rc, lines)
         for p in procs:
             p.join(60)
             assert p.exitcode == 0
