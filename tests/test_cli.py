@@ -168,6 +168,7 @@ def _ranked_worker(rank, world, port, argv, queue, pid=None, dump_s=None):
     from oracle_engine import OracleEngine
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
+    real_getpid = os.getpid
     if pid is not None:                       # each rank's default seed (:1149) differs
         os.getpid = lambda: pid + rank
     holder = {}
@@ -177,10 +178,16 @@ def _ranked_worker(rank, world, port, argv, queue, pid=None, dump_s=None):
         return holder["m"]
 
     lines = []
-    with contextlib.redirect_stdout(io.StringIO()):
-        rc = cli.main(argv + ["--gpus", str(world), "--backend", "gloo"], model_factory=factory,
-                      out=lines.append,
-                      engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links, B=n))
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            rc = cli.main(argv + ["--gpus", str(world), "--backend", "gloo"], model_factory=factory,
+                          out=lines.append,
+                          engine_factory=lambda n: OracleEngine(holder["m"].links, holder["m"].test_links, B=n))
+    finally:
+        # the real pid again before the queue is used: multiprocessing's queue decides from
+        # os.getpid() whether this process must flush its feeder thread at exit (with the fake pid
+        # both ranks sometimes exited 0 without their result reaching the parent)
+        os.getpid = real_getpid
     queue.put((rank, rc, lines))
 
 
